@@ -1,0 +1,210 @@
+/*
+ * vits_amd.h — C-ABI of the MI355X (gfx950) VITS hot path.
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t
+ * passed as `void*` (NULL = default stream).  No torch types cross this
+ * boundary; ownership of every buffer stays with the caller (the PyTorch
+ * caching allocator on the Python side).  All calls are asynchronous on the
+ * given stream, never synchronise the host, and return 0 on success or a
+ * negative VITS_E* code on a shape/argument error (checked on the host
+ * before anything is launched) or a hipError_t (positive) from the launch.
+ *
+ * Reference interfaces replaced (paths relative to emotional-vits/):
+ *   vits_maximum_path        monotonic_align.maximum_path, call site
+ *                            models.py:498 (external Cython package
+ *                            `monotonic-align`, not vendored)
+ *   vits_conv1d_forward      nn.Conv1d / ConvTranspose1d forward of
+ *                            modules.WN (modules.py:130-182),
+ *                            modules.ResBlock2 (modules.py:250-260),
+ *                            models.Generator (models.py:306-318),
+ *                            ResidualCouplingLayer.infer (modules.py:362-375)
+ *                            with their elementwise tails fused in
+ *   vits_linear_forward      per-utterance nn.Linear conditioning of
+ *                            WN.cond_layer (modules.py:109-110,139),
+ *                            ResBlock2.conds (modules.py:243-245,253),
+ *                            FFN2.cond (attentions.py:143,152)
+ *   vits_expand_prior        the prior-expansion matmuls + noise of
+ *                            SynthesizerTrn.infer_p2 (models.py:569-571)
+ *   vits_conv_post_tanh      Generator tail: leaky_relu(0.01) -> conv_post
+ *                            -> tanh (models.py:315-317)
+ *   vits_stft_mag_forward /  TorchSTFT.stft + STFTLoss.spec2mag
+ *   vits_stft_mag_backward   (modules.py:386-392, stft_loss.py:22-23)
+ *   vits_layer_norm_channels modules.LayerNorm (modules.py:41-44)
+ *   vits_attention_forward   MultiHeadAttention.attention core
+ *                            (attentions.py:85-100)
+ */
+#ifndef VITS_AMD_H
+#define VITS_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VITS_OK 0
+#define VITS_E_ARG (-1)     /* bad pointer / non-positive size */
+#define VITS_E_SHAPE (-2)   /* inconsistent shapes / strides */
+#define VITS_E_UNSUP (-3)   /* configuration outside the compiled kernels */
+
+/* ---------------------------------------------------------------------- */
+/* conv1d: implicit-GEMM dilated 1-D convolution on fp32 MFMA             */
+/* ---------------------------------------------------------------------- */
+
+/* epilogue kinds */
+#define VITS_EPI_STORE 0     /* y = act(acc + bias + cond) [+res] [accumulate] */
+#define VITS_EPI_GATE 1      /* y[p] = tanh(v[2p]) * sigmoid(v[2p+1])           */
+#define VITS_EPI_UPSAMPLE 2  /* polyphase ConvTranspose1d output scatter        */
+
+/* activations applied to v before residual/accumulate (STORE epilogue) */
+#define VITS_ACT_NONE 0
+#define VITS_ACT_RELU 1
+#define VITS_ACT_TANH 2
+
+/* tile configurations (rows x cols of one workgroup) */
+#define VITS_TILE_128x128 0
+#define VITS_TILE_64x256 1
+#define VITS_TILE_32x256 2
+
+typedef struct vits_conv_out {
+  float* y;               /* output [B][*][y_cstride]                        */
+  int64_t y_bstride;      /* elements between utterances                     */
+  int32_t y_cstride;      /* elements between channels                       */
+  int32_t act;            /* VITS_ACT_*                                      */
+  const float* res;       /* optional residual (may alias y)                 */
+  int64_t res_bstride;
+  int32_t res_cstride;
+  float res_scale;        /* y = res + res_scale * v                         */
+  int32_t accumulate;     /* y = y_old + (...)                               */
+  float post_div;         /* y /= post_div when != 1                         */
+} vits_conv_out;
+
+typedef struct vits_conv1d_desc {
+  /* input x: [B][cin][*], element (b, c, t) at b*x_bstride + c*x_cstride + t */
+  const float* x;
+  int64_t x_bstride;
+  int32_t x_cstride;
+  int32_t cin;
+  int32_t tin;            /* valid input positions; outside reads as 0        */
+  float in_slope;         /* prologue leaky-relu slope on x; 1.0 = identity   */
+  /* packed weights: [cin_pad][k][m_pad] fp32, see vits_amd/engine.py       */
+  const float* w;
+  int32_t m;              /* GEMM rows actually produced                      */
+  int32_t m_pad;          /* row stride of the packed weights                 */
+  int32_t cin_pad;        /* multiple of kc                                    */
+  int32_t kc;             /* input channels staged per K-chunk (even)         */
+  int32_t k;              /* taps                                             */
+  int32_t dil;            /* tap dilation                                      */
+  int32_t pad_left;       /* input position of column n, tap j: n-pad+j*dil   */
+  int32_t n_out;          /* GEMM columns (output positions)                  */
+  int32_t tile;           /* VITS_TILE_*                                      */
+  /* epilogue */
+  int32_t epi;            /* VITS_EPI_*                                       */
+  const float* bias;      /* logical-order bias or NULL                       */
+  const float* cond;      /* [B][cond_bstride] logical-order add, or NULL     */
+  int64_t cond_bstride;
+  int32_t split;          /* STORE: rows [0,split)->out0, [split,m)->out1     */
+  int32_t up_u;           /* UPSAMPLE: stride u                               */
+  int32_t up_pad;         /* UPSAMPLE: ConvTranspose padding                  */
+  int32_t t_out;          /* UPSAMPLE: output length                          */
+  const int32_t* lengths; /* [B]: zero output columns t >= lengths[b]; NULL   */
+  vits_conv_out out0;
+  vits_conv_out out1;
+} vits_conv1d_desc;
+
+int vits_conv1d_forward(const vits_conv1d_desc* d, int batch, void* stream);
+
+/* Run `n` conv descriptors back to back on one stream (one host call). */
+int vits_conv1d_forward_seq(const vits_conv1d_desc* d, int n, int batch, void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* per-utterance conditioning GEMV: y[b][n] = W[n][:] . g[b][:] + bias[n] */
+/* ---------------------------------------------------------------------- */
+int vits_linear_forward(const float* g, int64_t g_bstride, const float* w, const float* bias,
+                        float* y, int64_t y_bstride, int batch, int n_out, int n_in,
+                        void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* prior expansion: z[b][c][t] = sum_x attn[b][t][x] m[b][c][x]           */
+/*                    + noise[b][c][t] * sum_x attn[b][t][x] s[b][c][x]   */
+/* ---------------------------------------------------------------------- */
+int vits_expand_prior(const float* attn, const float* m, const float* s, const float* noise,
+                      float* z, int batch, int channels, int t_y, int t_x, void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* Generator tail: y[b][t] = tanh(sum_{c,j} w[c][j] lrelu(x[b][c][t-3+j], 0.01)) */
+/* w: [channels][7] (conv_post, no bias)                                  */
+/* ---------------------------------------------------------------------- */
+int vits_conv_post_tanh(const float* x, int64_t x_bstride, int32_t x_cstride, const float* w,
+                        float* y, int batch, int channels, int t_len, int ksize, void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* Monotonic alignment search (VITS DP + backtrack), bit-exact vs the     */
+/* Cython core.  neg_cent [B][t_t][t_s] fp32 (the reference casts to fp32 */
+/* before the DP); mask [B][t_t][t_s] of mask_dtype: lengths are taken as */
+/* t_t[b] = sum_y mask[b][y][0], t_s[b] = sum_x mask[b][0][x] exactly as  */
+/* monotonic_align/__init__.py does.  path [B][t_t][t_s] of path_dtype is */
+/* written in full (1 on the path, 0 elsewhere).                          */
+/* dtype codes: VITS_DT_*.                                                */
+/* ---------------------------------------------------------------------- */
+#define VITS_DT_F32 0
+#define VITS_DT_F16 1
+#define VITS_DT_BF16 2
+#define VITS_DT_I32 3
+int vits_maximum_path(const float* neg_cent, const void* mask, int mask_dtype, void* path,
+                      int path_dtype, int batch, int t_t, int t_s, void* workspace,
+                      int64_t workspace_bytes, void* stream);
+/* same, with explicit per-utterance lengths (int32 [B] each, on device) */
+int vits_maximum_path_lengths(const float* neg_cent, const int32_t* t_t_len,
+                              const int32_t* t_s_len, void* path, int path_dtype, int batch,
+                              int t_t, int t_s, void* workspace, int64_t workspace_bytes,
+                              void* stream);
+/* bytes of workspace the two calls above need (0 when the backtrack bits */
+/* fit in LDS)                                                            */
+int64_t vits_maximum_path_workspace(int batch, int t_t, int t_s);
+
+/* ---------------------------------------------------------------------- */
+/* STFT magnitude and its adjoint.  x [B][L] fp32; the signal is reflect- */
+/* padded by `pad` samples on both sides (pad = n_fft/2 reproduces        */
+/* torch.stft(center=True, pad_mode='reflect'); mel_processing pads       */
+/* (n_fft-hop)/2 itself and calls center=False), then framed with `hop`,  */
+/* windowed by `window` (length win, centred in n_fft as torch.stft does) */
+/* and transformed: frames = (L + 2 pad - n_fft)/hop + 1.                 */
+/* mag [B][n_fft/2+1][frames] = sqrt(re^2 + im^2 + eps); re/im (optional, */
+/* needed by the backward) same layout.                                   */
+/* ---------------------------------------------------------------------- */
+int vits_stft_mag_forward(const float* x, int batch, int length, const float* window,
+                          int n_fft, int hop, int win, int pad, float eps, float* mag,
+                          float* re, float* im, void* stream);
+/* grad_x [B][L] = d(sum grad_mag * mag)/dx.  workspace: frames*n_fft*B   */
+/* floats (vits_stft_workspace).                                          */
+int vits_stft_mag_backward(const float* grad_mag, const float* mag, const float* re,
+                           const float* im, const float* window, int batch, int length,
+                           int n_fft, int hop, int win, int pad, float* grad_x,
+                           float* workspace, int64_t workspace_floats, void* stream);
+int64_t vits_stft_workspace(int batch, int length, int n_fft, int hop, int pad);
+
+/* ---------------------------------------------------------------------- */
+/* channel LayerNorm over dim 1 of [B][C][T] (+ optional residual input)  */
+/* y = LN(x + r) * gamma + beta; eps as given                             */
+/* ---------------------------------------------------------------------- */
+int vits_layer_norm_channels(const float* x, const float* r, const float* gamma,
+                             const float* beta, float* y, int batch, int channels, int t_len,
+                             float eps, const int32_t* lengths, void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* scaled-dot-product attention over [B][H*D][T] channel-major q/k/v,     */
+/* key mask from lengths (fill -1e4), out [B][H*D][T]                      */
+/* ---------------------------------------------------------------------- */
+int vits_attention_forward(const float* q, const float* k, const float* v, float* out,
+                           int batch, int heads, int head_dim, int t_len,
+                           int64_t bstride, const int32_t* lengths, void* stream);
+
+/* library introspection */
+const char* vits_amd_version(void);
+int vits_amd_device_arch(char* buf, int len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VITS_AMD_H */

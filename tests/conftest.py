@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and libvits_amd.so")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+def _gpu_available():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def device():
+    import torch
+
+    if not _gpu_available():
+        pytest.skip("no ROCm GPU")
+    return torch.device("cuda:0")

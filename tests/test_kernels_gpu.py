@@ -1,0 +1,231 @@
+"""Kernel-level parity of libvits_amd against CPU fp32 references.
+
+Floating-point ops are compared against torch CPU fp32 (the same library the
+reference runs on) with tolerances stated per test; MAS is compared bit-exactly
+against the C oracle (oracle/mas_oracle.c)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from vits_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-4  # fp32 MFMA vs CPU fp32: different summation order only
+
+
+def _close(a, b, tol=RTOL, what=""):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    scale = b.abs().max().item() + 1e-12
+    err = (a - b).abs().max().item()
+    assert err <= tol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("B,cin,cout,k,dil,T", [
+    (1, 16, 32, 3, 1, 50), (2, 192, 512, 7, 1, 101), (3, 256, 256, 11, 5, 300),
+    (2, 64, 64, 7, 3, 1000), (2, 16, 32, 11, 1, 777), (1, 513, 256, 1, 1, 64),
+    (2, 256, 96, 1, 1, 130), (1, 96, 256, 1, 1, 33), (2, 32, 32, 3, 5, 2000),
+])
+def test_conv1d_store(device, B, cin, cout, k, dil, T):
+    g = torch.Generator().manual_seed(B * 1000 + cin + k)
+    x = torch.randn(B, cin, T, generator=g)
+    w = torch.randn(cout, cin, k, generator=g) / (cin * k) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    pad = (k * dil - dil) // 2
+    ref = F.conv1d(F.leaky_relu(x, 0.1), w, b, padding=pad, dilation=dil)
+    res = torch.randn(B, cout, T, generator=g)
+    ref = ref + res
+    layer = ops.pack_conv(w.to(device), b.to(device), dilation=dil)
+    out = ops.conv1d(x.to(device), layer, in_slope=0.1, residual=res.to(device))
+    _close(out, ref, what="conv1d")
+
+
+@pytest.mark.parametrize("B,C,k,dil,T", [(2, 256, 3, 1, 200), (1, 32, 11, 5, 900), (2, 128, 7, 3, 333)])
+def test_conv1d_gate_cond(device, B, C, k, dil, T):
+    g = torch.Generator().manual_seed(7 + C)
+    x = torch.randn(B, C, T, generator=g)
+    w = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
+    b = torch.randn(C, generator=g) * 0.1
+    cond = torch.randn(B, C, generator=g)
+    pad = (k * dil - dil) // 2
+    xt = F.conv1d(F.leaky_relu(x, 0.1), w, b, padding=pad, dilation=dil)
+    xa, xb = xt.chunk(2, 1)
+    sa, sb = cond.chunk(2, 1)
+    ref = torch.tanh(xa + sa.unsqueeze(-1)) * torch.sigmoid(xb + sb.unsqueeze(-1))
+    layer = ops.pack_conv(w.to(device), b.to(device), dilation=dil, gate=True)
+    out = ops.conv1d(x.to(device), layer, in_slope=0.1, cond=cond.to(device))
+    _close(out, ref, what="gate")
+
+
+@pytest.mark.parametrize("B,cin,cout,K,u,T", [(1, 512, 256, 16, 8, 40), (2, 256, 128, 12, 6, 37),
+                                             (2, 128, 64, 4, 2, 301), (1, 64, 32, 4, 2, 1000)])
+def test_conv_transpose_polyphase(device, B, cin, cout, K, u, T):
+    g = torch.Generator().manual_seed(K + cin)
+    x = torch.randn(B, cin, T, generator=g)
+    w = torch.randn(cin, cout, K, generator=g) / (cin * 2) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    pad = (K - u) // 2
+    ref = F.conv_transpose1d(F.leaky_relu(x, 0.1), w, b, stride=u, padding=pad)
+    layer = ops.pack_conv_transpose(w.to(device), b.to(device), u, pad)
+    out = ops.conv1d(x.to(device), layer, in_slope=0.1)
+    _close(out, ref, what="convT")
+
+
+def test_conv1d_masked_split_accumulate(device):
+    B, H, T = 3, 64, 150
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(B, H, T, generator=g)
+    w = torch.randn(2 * H, H, 1, generator=g) / H ** 0.5
+    b = torch.randn(2 * H, generator=g) * 0.1
+    x = torch.randn(B, H, T, generator=g)
+    acc0 = torch.randn(B, H, T, generator=g)
+    lengths = torch.tensor([150, 97, 1], dtype=torch.int32)
+    mask = (torch.arange(T)[None] < lengths[:, None]).float().unsqueeze(1)
+    rs = F.conv1d(a, w, b)
+    ref_x = (x + rs[:, :H]) * mask
+    ref_o = acc0 + rs[:, H:]
+    dev = device
+    layer = ops.pack_conv(w.to(dev), b.to(dev))
+    xd, od, ad = x.to(dev).clone(), acc0.to(dev).clone(), a.to(dev)
+    o0 = ops.make_out(xd, res=xd)
+    o1 = ops.make_out(od, accumulate=True)
+    d = ops.make_desc(layer, ad, o0, out1=o1, split=H, lengths=lengths.to(dev))
+    ops.conv1d_launch(d, B, ad.device)
+    _close(xd, ref_x, what="residual half")
+    # out1 is not masked by the kernel: the reference masks output once at the end
+    o1ref = ref_o.clone()
+    o1ref[mask.expand_as(o1ref) == 0] = 0
+    got = od.cpu()
+    got[mask.expand_as(got) == 0] = 0
+    _close(got, o1ref, what="skip half")
+
+
+def test_linear_rows(device):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(5, 1024, generator=g)
+    w = torch.randn(3000, 1024, generator=g) * 0.03
+    b = torch.randn(3000, generator=g)
+    out = ops.linear_rows(x.to(device), w.to(device), b.to(device))
+    _close(out, F.linear(x, w, b), what="linear")
+
+
+def test_expand_prior(device):
+    g = torch.Generator().manual_seed(9)
+    B, Cc, Tx = 2, 192, 37
+    dur = torch.randint(1, 6, (B, 1, Tx), generator=g).float()
+    Ty = int(dur.sum(-1).max())
+    cum = torch.cumsum(dur, -1)
+    t = torch.arange(Ty).float()
+    path = (t[None, :, None] < cum[:, 0, None, :]).float()
+    path = path - F.pad(path, (1, 0))[:, :, :-1]
+    attn = path  # [B, Ty, Tx]
+    m = torch.randn(B, Cc, Tx, generator=g)
+    s = torch.rand(B, Cc, Tx, generator=g) + 0.5
+    n = torch.randn(B, Cc, Ty, generator=g)
+    ref = torch.matmul(attn, m.transpose(1, 2)).transpose(1, 2) + n * torch.matmul(attn, s.transpose(1, 2)).transpose(1, 2)
+    out = ops.expand_prior(attn.to(device), m.to(device), s.to(device), n.to(device))
+    _close(out, ref, tol=1e-6, what="expand")
+
+
+def test_conv_post_tanh(device):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 32, 1234, generator=g)
+    w = torch.randn(1, 32, 7, generator=g) * 0.2
+    ref = torch.tanh(F.conv1d(F.leaky_relu(x), w, None, padding=3))
+    out = ops.conv_post_tanh(x.to(device), w.to(device))
+    _close(out, ref, what="conv_post")
+
+
+@pytest.mark.parametrize("B,Tt,Ts", [(4, 60, 13), (3, 500, 100), (2, 1000, 384), (1, 7, 7), (2, 300, 65)])
+def test_maximum_path_bitexact(device, B, Tt, Ts):
+    from oracle import mas as mas_oracle
+
+    rng = np.random.default_rng(Tt * 7 + Ts)
+    nc = rng.standard_normal((B, Tt, Ts)).astype(np.float32) * 3
+    t_t = rng.integers(max(1, Tt // 2), Tt + 1, size=B).astype(np.int32)
+    t_t[0] = Tt
+    t_s = np.minimum(rng.integers(1, Ts + 1, size=B), t_t).astype(np.int32)
+    t_s[0] = min(Ts, Tt)
+    mask = np.zeros((B, Tt, Ts), np.float32)
+    for b in range(B):
+        mask[b, :t_t[b], :t_s[b]] = 1
+    ref = mas_oracle.maximum_path(nc, mask)
+    out = ops.maximum_path(torch.from_numpy(nc).to(device), torch.from_numpy(mask).to(device))
+    assert out.dtype == torch.float32
+    assert np.array_equal(out.cpu().numpy().astype(np.int32), ref)
+
+
+def test_maximum_path_ties_and_dtype(device):
+    from oracle import mas as mas_oracle
+
+    # integer-valued scores create many exact ties: the strict '<' rule decides
+    rng = np.random.default_rng(1)
+    nc = rng.integers(-2, 3, size=(3, 40, 12)).astype(np.float32)
+    mask = np.ones_like(nc)
+    ref = mas_oracle.maximum_path(nc, mask)
+    out = ops.maximum_path(torch.from_numpy(nc).to(device).half(), torch.from_numpy(mask).to(device))
+    assert out.dtype == torch.float16
+    assert np.array_equal(out.float().cpu().numpy().astype(np.int32), ref)
+
+
+@pytest.mark.parametrize("n_fft,hop", [(128, 32), (256, 64), (512, 128), (1024, 256), (2048, 512)])
+def test_stft_mag_fwd_bwd(device, n_fft, hop):
+    g = torch.Generator().manual_seed(n_fft)
+    x = (torch.randn(3, 9216, generator=g) * 0.3).clamp(-1, 1)
+    win = torch.hann_window(n_fft)
+    xr = x.clone().requires_grad_(True)
+    spec = torch.stft(xr, n_fft, hop, n_fft, win, center=True, pad_mode="reflect", return_complex=True)
+    ref = torch.sqrt(spec.real ** 2 + spec.imag ** 2 + 1e-7)
+    gm = torch.randn(ref.shape, generator=g)
+    (ref * gm).sum().backward()
+    xd = x.to(device).requires_grad_(True)
+    out = ops.stft_mag(xd, win.to(device), n_fft, hop, n_fft)
+    _close(out, ref, tol=2e-5, what="stft mag")
+    (out * gm.to(device)).sum().backward()
+    _close(xd.grad, xr.grad, tol=2e-5, what="stft grad")
+
+
+def test_stft_spectrogram_args(device):
+    # mel_processing.spectrogram_torch: pad (n_fft-hop)/2 reflect, win 768 centred in 1024
+    g = torch.Generator().manual_seed(2)
+    y = (torch.randn(2, 19200, generator=g) * 0.3).clamp(-1, 1)
+    n_fft, hop, win = 1024, 192, 768
+    p = (n_fft - hop) // 2
+    yp = F.pad(y.unsqueeze(1), (p, p), mode="reflect").squeeze(1)
+    spec = torch.stft(yp, n_fft, hop, win, torch.hann_window(win), center=False, return_complex=True)
+    ref = torch.sqrt(spec.real ** 2 + spec.imag ** 2 + 1e-6)
+    out = ops.stft_mag(y.to(device), torch.hann_window(win).to(device), n_fft, hop, win, pad=p, eps=1e-6)
+    _close(out, ref, tol=2e-5, what="spectrogram")
+
+
+def test_layer_norm_channels(device):
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 256, 77, generator=g)
+    r = torch.randn(3, 256, 77, generator=g)
+    gamma = torch.randn(256, generator=g)
+    beta = torch.randn(256, generator=g)
+    ref = F.layer_norm((x + r).transpose(1, -1), (256,), gamma, beta, 1e-5).transpose(1, -1)
+    out = ops.layer_norm_channels(x.to(device), gamma.to(device), beta.to(device), residual=r.to(device))
+    _close(out, ref, tol=1e-5, what="LN")
+
+
+@pytest.mark.parametrize("T,lens", [(100, [100]), (77, [77, 50, 3]), (500, [500, 321])])
+def test_attention(device, T, lens):
+    g = torch.Generator().manual_seed(T)
+    B, H, D = len(lens), 2, 128
+    q = torch.randn(B, H * D, T, generator=g)
+    k = torch.randn(B, H * D, T, generator=g)
+    v = torch.randn(B, H * D, T, generator=g)
+    lengths = torch.tensor(lens, dtype=torch.int32)
+    mask = (torch.arange(T)[None] < lengths[:, None]).float()
+    am = (mask.unsqueeze(2) * mask.unsqueeze(1)).unsqueeze(1)
+    qh = q.view(B, H, D, T).transpose(2, 3)
+    kh = k.view(B, H, D, T).transpose(2, 3)
+    vh = v.view(B, H, D, T).transpose(2, 3)
+    sc = torch.matmul(qh / D ** 0.5, kh.transpose(-2, -1)).masked_fill(am == 0, -1e4)
+    ref = torch.matmul(F.softmax(sc, -1), vh).transpose(2, 3).reshape(B, H * D, T)
+    out = ops.attention(q.to(device), k.to(device), v.to(device), H, lengths=lengths.to(device))
+    _close(out, ref, tol=2e-5, what="attention")

@@ -1,0 +1,165 @@
+"""ctypes binding of libvits_amd.so (the C-ABI declared in include/vits_amd.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (Makefile in
+``vits_amd/csrc``) into ``vits_amd/lib/libvits_amd.so``.  There is no
+fallback: if the library is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libvits_amd.so")
+_lock = threading.Lock()
+_lib = None
+
+VITS_OK = 0
+VITS_E_ARG = -1
+VITS_E_SHAPE = -2
+VITS_E_UNSUP = -3
+
+EPI_STORE, EPI_GATE, EPI_UPSAMPLE = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
+TILE_128x128, TILE_64x256, TILE_32x256 = 0, 1, 2
+TILE_ROWS = {TILE_128x128: 128, TILE_64x256: 64, TILE_32x256: 32}
+DT_F32, DT_F16, DT_BF16, DT_I32 = 0, 1, 2, 3
+
+
+class ConvOut(C.Structure):
+    _fields_ = [
+        ("y", C.c_void_p),
+        ("y_bstride", C.c_int64),
+        ("y_cstride", C.c_int32),
+        ("act", C.c_int32),
+        ("res", C.c_void_p),
+        ("res_bstride", C.c_int64),
+        ("res_cstride", C.c_int32),
+        ("res_scale", C.c_float),
+        ("accumulate", C.c_int32),
+        ("post_div", C.c_float),
+    ]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p),
+        ("x_bstride", C.c_int64),
+        ("x_cstride", C.c_int32),
+        ("cin", C.c_int32),
+        ("tin", C.c_int32),
+        ("in_slope", C.c_float),
+        ("w", C.c_void_p),
+        ("m", C.c_int32),
+        ("m_pad", C.c_int32),
+        ("cin_pad", C.c_int32),
+        ("kc", C.c_int32),
+        ("k", C.c_int32),
+        ("dil", C.c_int32),
+        ("pad_left", C.c_int32),
+        ("n_out", C.c_int32),
+        ("tile", C.c_int32),
+        ("epi", C.c_int32),
+        ("bias", C.c_void_p),
+        ("cond", C.c_void_p),
+        ("cond_bstride", C.c_int64),
+        ("split", C.c_int32),
+        ("up_u", C.c_int32),
+        ("up_pad", C.c_int32),
+        ("t_out", C.c_int32),
+        ("lengths", C.c_void_p),
+        ("out0", ConvOut),
+        ("out1", ConvOut),
+    ]
+
+
+_SIGS = {
+    "vits_conv1d_forward": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_void_p]),
+    "vits_conv1d_forward_seq": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_int, C.c_void_p]),
+    "vits_linear_forward": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int,
+         C.c_int, C.c_void_p],
+    ),
+    "vits_expand_prior": (
+        C.c_int,
+        [C.c_void_p] * 5 + [C.c_int] * 4 + [C.c_void_p],
+    ),
+    "vits_conv_post_tanh": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+         C.c_int, C.c_void_p],
+    ),
+    "vits_maximum_path": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+         C.c_void_p, C.c_int64, C.c_void_p],
+    ),
+    "vits_maximum_path_lengths": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+         C.c_void_p, C.c_int64, C.c_void_p],
+    ),
+    "vits_maximum_path_workspace": (C.c_int64, [C.c_int, C.c_int, C.c_int]),
+    "vits_stft_mag_forward": (
+        C.c_int,
+        [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
+         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+    ),
+    "vits_stft_mag_backward": (
+        C.c_int,
+        [C.c_void_p] * 5
+        + [C.c_int] * 6
+        + [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p],
+    ),
+    "vits_stft_workspace": (C.c_int64, [C.c_int] * 5),
+    "vits_layer_norm_channels": (
+        C.c_int,
+        [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_float, C.c_void_p, C.c_void_p],
+    ),
+    "vits_attention_forward": (
+        C.c_int,
+        [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_int64, C.c_void_p, C.c_void_p],
+    ),
+    "vits_amd_version": (C.c_char_p, []),
+    "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS.keys())
+
+
+class VitsAmdError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load():
+    """Load (once) and return the ctypes library; raises if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            raise VitsAmdError(
+                f"libvits_amd.so not found at {_LIB_PATH}; run __graft_entry__.build() "
+                "(make -C vits_amd/csrc). There is no CPU fallback."
+            )
+        lib = C.CDLL(_LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != VITS_OK:
+        kind = {VITS_E_ARG: "bad argument", VITS_E_SHAPE: "shape mismatch",
+                VITS_E_UNSUP: "unsupported configuration"}.get(rc, f"HIP error {rc}")
+        raise VitsAmdError(f"{what}: {kind} (rc={rc})")

@@ -1,0 +1,206 @@
+// misc.hip — small per-utterance / elementwise kernels around the conv stacks.
+//
+//   vits_linear_forward   per-utterance conditioning GEMV (all cond Linears
+//                         of one forward stacked into one weight matrix):
+//                         modules.py:109-110,139 (WN.cond_layer),
+//                         modules.py:243-245,253 (ResBlock2.conds),
+//                         attentions.py:143,152 (FFN2.cond),
+//                         models.py:37-38,49-52 (DurationPredictor.cond1/2)
+//   vits_expand_prior     attn-weighted prior expansion + reparameterised
+//                         noise, models.py:569-571 (infer_p2)
+//   vits_conv_post_tanh   Generator tail, models.py:315-317
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// GEMV: one wave per output row n; the row of W (n_in floats) is read once
+// with 16-byte loads and reused for every utterance in the batch.  g rows are
+// L2-resident (batch x n_in floats).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restrict__ g,
+                                                          int64_t g_bstride,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ y, int64_t y_bstride,
+                                                          int batch, int n_out, int n_in) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= n_out) return;
+  const float* wr = w + (int64_t)n * n_in;
+  const float bv = bias ? bias[n] : 0.f;
+  for (int b = 0; b < batch; ++b) {
+    const float* gr = g + (int64_t)b * g_bstride;
+    float s = 0.f;
+    if ((n_in & 3) == 0) {
+      for (int i = lane * 4; i < n_in; i += 256) {
+        const float4 wv = *reinterpret_cast<const float4*>(wr + i);
+        const float4 gv = *reinterpret_cast<const float4*>(gr + i);
+        s += wv.x * gv.x + wv.y * gv.y + wv.z * gv.z + wv.w * gv.w;
+      }
+    } else {
+      for (int i = lane; i < n_in; i += 64) s += wr[i] * gr[i];
+    }
+    s = wave_sum(s);
+    if (lane == 0) y[(int64_t)b * y_bstride + n] = s + bv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// prior expansion.  Workgroup = (utterance b, 64 frames).  Each wave owns 16
+// frames; for a frame it ballots the non-zero attention weights over t_x
+// (one-hot in practice, but any weights are summed in x order, matching a
+// sequential dot product) and accumulates m and s rows for all channels into
+// an LDS tile that is then written out with the frame index contiguous.
+// ---------------------------------------------------------------------------
+constexpr int EP_T = 64;
+
+__global__ __launch_bounds__(256) void expand_prior_kernel(const float* __restrict__ attn,
+                                                           const float* __restrict__ m,
+                                                           const float* __restrict__ s,
+                                                           const float* __restrict__ noise,
+                                                           float* __restrict__ z, int channels,
+                                                           int t_y, int t_x) {
+  extern __shared__ float tile[];  // [2][channels][EP_T+1]
+  float* tm = tile;
+  float* ts = tile + channels * (EP_T + 1);
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * EP_T;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const float* ab = attn + (int64_t)b * t_y * t_x;
+  const float* mb = m + (int64_t)b * channels * t_x;
+  const float* sb = s + (int64_t)b * channels * t_x;
+
+  for (int tl = wid; tl < EP_T; tl += 4) {
+    const int t = t0 + tl;
+    // per-lane channel accumulators (channels <= 64*CPL)
+    float am[4] = {0.f, 0.f, 0.f, 0.f};
+    float as_[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t < t_y) {
+      const float* ar = ab + (int64_t)t * t_x;
+      for (int x0 = 0; x0 < t_x; x0 += 64) {
+        const int x = x0 + lane;
+        const float av = x < t_x ? ar[x] : 0.f;
+        unsigned long long nz = __ballot(av != 0.f);
+        while (nz) {
+          const int bit = __ffsll((long long)nz) - 1;
+          nz &= nz - 1;
+          const float a = __shfl(av, bit, 64);
+          const int xx = x0 + bit;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = lane + 64 * q;
+            if (c < channels) {
+              am[q] += a * mb[(int64_t)c * t_x + xx];
+              as_[q] += a * sb[(int64_t)c * t_x + xx];
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = lane + 64 * q;
+      if (c < channels) {
+        tm[c * (EP_T + 1) + tl] = am[q];
+        ts[c * (EP_T + 1) + tl] = as_[q];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < channels * EP_T; i += 256) {
+    const int c = i / EP_T;
+    const int tl = i - c * EP_T;
+    const int t = t0 + tl;
+    if (t < t_y) {
+      const int64_t o = ((int64_t)b * channels + c) * t_y + t;
+      z[o] = tm[c * (EP_T + 1) + tl] + noise[o] * ts[c * (EP_T + 1) + tl];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generator tail: one thread per output sample; the input window of the
+// workgroup ([channels][256 + k - 1]) is staged in LDS with the 0.01 leaky
+// relu applied once per element.
+// ---------------------------------------------------------------------------
+constexpr int CP_T = 256;
+
+__global__ __launch_bounds__(256) void conv_post_tanh_kernel(const float* __restrict__ x,
+                                                             int64_t x_bstride, int x_cstride,
+                                                             const float* __restrict__ w,
+                                                             float* __restrict__ y, int channels,
+                                                             int t_len, int ksize) {
+  extern __shared__ float sm[];  // [channels][CP_T + ksize - 1] then w
+  const int W = CP_T + ksize - 1;
+  float* xs = sm;
+  float* wsm = sm + channels * W;
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * CP_T;
+  const int pad = (ksize - 1) / 2;
+  const float* xb = x + (int64_t)b * x_bstride;
+  for (int i = threadIdx.x; i < channels * ksize; i += 256) wsm[i] = w[i];
+  for (int c = 0; c < channels; ++c) {
+    for (int t = threadIdx.x; t < W; t += 256) {
+      const int tt = t0 - pad + t;
+      float v = 0.f;
+      if (tt >= 0 && tt < t_len) {
+        v = xb[(int64_t)c * x_cstride + tt];
+        v = v < 0.f ? 0.01f * v : v;
+      }
+      xs[c * W + t] = v;
+    }
+  }
+  __syncthreads();
+  const int tl = threadIdx.x;
+  const int t = t0 + tl;
+  if (t >= t_len) return;
+  float acc = 0.f;
+  for (int c = 0; c < channels; ++c) {
+    const float* xr = xs + c * W + tl;
+    const float* wr = wsm + c * ksize;
+    for (int j = 0; j < ksize; ++j) acc += wr[j] * xr[j];
+  }
+  y[(int64_t)b * t_len + t] = tanhf(acc);
+}
+
+}  // namespace
+
+extern "C" int vits_linear_forward(const float* g, int64_t g_bstride, const float* w,
+                                   const float* bias, float* y, int64_t y_bstride, int batch,
+                                   int n_out, int n_in, void* stream) {
+  VITS_CHECK_ARG(g && w && y && batch > 0 && n_out > 0 && n_in > 0);
+  if ((n_in & 3) == 0)
+    VITS_CHECK_SHAPE(((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(g)) & 15) == 0 &&
+                     (g_bstride & 3) == 0);
+  dim3 grid((n_out + 3) / 4);
+  hipLaunchKernelGGL(linear_rows_kernel, grid, dim3(256), 0, as_stream(stream), g, g_bstride, w,
+                     bias, y, y_bstride, batch, n_out, n_in);
+  return vits_launch_status();
+}
+
+extern "C" int vits_expand_prior(const float* attn, const float* m, const float* s,
+                                 const float* noise, float* z, int batch, int channels, int t_y,
+                                 int t_x, void* stream) {
+  VITS_CHECK_ARG(attn && m && s && noise && z && batch > 0 && channels > 0 && t_y > 0 && t_x > 0);
+  VITS_CHECK_SHAPE(channels <= 256);
+  const size_t lds = sizeof(float) * 2 * channels * (EP_T + 1);
+  dim3 grid((t_y + EP_T - 1) / EP_T, batch);
+  hipLaunchKernelGGL(expand_prior_kernel, grid, dim3(256), lds, as_stream(stream), attn, m, s,
+                     noise, z, channels, t_y, t_x);
+  return vits_launch_status();
+}
+
+extern "C" int vits_conv_post_tanh(const float* x, int64_t x_bstride, int32_t x_cstride,
+                                   const float* w, float* y, int batch, int channels, int t_len,
+                                   int ksize, void* stream) {
+  VITS_CHECK_ARG(x && w && y && batch > 0 && channels > 0 && t_len > 0 && ksize > 0);
+  VITS_CHECK_SHAPE((ksize & 1) == 1 && x_cstride >= t_len);
+  const size_t lds = sizeof(float) * ((size_t)channels * (CP_T + ksize - 1) + channels * ksize);
+  VITS_CHECK_SHAPE(lds <= 64 * 1024);
+  dim3 grid((t_len + CP_T - 1) / CP_T, batch);
+  hipLaunchKernelGGL(conv_post_tanh_kernel, grid, dim3(256), lds, as_stream(stream), x,
+                     x_bstride, x_cstride, w, y, channels, t_len, ksize);
+  return vits_launch_status();
+}

@@ -1,0 +1,446 @@
+"""Tensor-level wrappers over the C-ABI (libvits_amd.so).
+
+Every function here requires CUDA(ROCm) tensors and launches HIP kernels on
+the current torch stream; there is no CPU path (a CPU tensor raises).
+Weight packing helpers turn reference-layout conv weights into the
+``[cin_pad][k][m_pad]`` slabs the MFMA conv kernel streams.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import (ACT_NONE, ConvDesc, ConvOut, EPI_GATE, EPI_STORE, EPI_UPSAMPLE, TILE_128x128,
+                   TILE_32x256, TILE_64x256, TILE_ROWS, check)
+
+# ---------------------------------------------------------------------------
+# plumbing
+# ---------------------------------------------------------------------------
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(*tensors: torch.Tensor):
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise _lib.VitsAmdError(
+                "vits_amd HIP ops need tensors on a ROCm GPU (device 'cuda'); "
+                f"got {t.device}. There is no CPU path.")
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def weight_norm_effective(module: torch.nn.Module, name: str = "weight") -> torch.Tensor:
+    """Effective weight of a (legacy) weight-normed or plain layer."""
+    g = getattr(module, name + "_g", None)
+    v = getattr(module, name + "_v", None)
+    if g is not None and v is not None:
+        return torch._weight_norm(v, g, 0)
+    return getattr(module, name)
+
+
+# ---------------------------------------------------------------------------
+# conv layer packing
+# ---------------------------------------------------------------------------
+
+
+def _pick_tile(m: int) -> int:
+    if m > 64:
+        return TILE_128x128
+    if m > 32:
+        return TILE_64x256
+    return TILE_32x256
+
+
+def _pick_kc(cin: int, k: int, bm: int) -> int:
+    budget = max(2, (8192 // bm) // k)  # kc * k * BM * 4 bytes <= 32 KiB
+    kc = min(32, budget, cin + (cin & 1))
+    kc = max(2, kc - (kc & 1))
+    return kc
+
+
+@dataclass
+class PackedConv:
+    """A conv (or polyphase conv-transpose) lowered for vits_conv1d_forward."""
+
+    w: torch.Tensor            # [cin_pad, k, m_pad] fp32 contiguous
+    bias: Optional[torch.Tensor]
+    cin: int
+    m: int                     # GEMM rows
+    k: int
+    dil: int
+    pad_left: int
+    epi: int
+    tile: int
+    kc: int
+    up_u: int = 1
+    up_pad: int = 0
+    out_channels: int = 0      # channels of the produced tensor
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def m_pad(self) -> int:
+        return self.w.shape[2]
+
+    @property
+    def cin_pad(self) -> int:
+        return self.w.shape[0]
+
+
+def _finish_pack(rows_w: torch.Tensor, k: int, tile: int) -> tuple[torch.Tensor, int]:
+    """rows_w: [m, cin, k] -> packed [cin_pad, k, m_pad]."""
+    m, cin, _ = rows_w.shape
+    kc = _pick_kc(cin, k, TILE_ROWS[tile])
+    cin_pad = (cin + kc - 1) // kc * kc
+    m_pad = (m + 127) // 128 * 128
+    packed = rows_w.new_zeros(cin_pad, k, m_pad, dtype=torch.float32)
+    packed[:cin, :, :m] = rows_w.permute(1, 2, 0).to(torch.float32)
+    return packed.contiguous(), kc
+
+
+def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], *, dilation: int = 1,
+              padding: Optional[int] = None, gate: bool = False) -> PackedConv:
+    """nn.Conv1d weight [Cout, Cin, k].  ``gate``: rows (a_p, b_p) interleaved
+    so the tanh/sigmoid pair of output p lands in one lane (EPI_GATE)."""
+    w = weight.detach().to(torch.float32)
+    cout, cin, k = w.shape
+    if padding is None:
+        padding = (k * dilation - dilation) // 2
+    if gate:
+        assert cout % 2 == 0
+        h = cout // 2
+        rows = torch.stack([w[:h], w[h:]], dim=1).reshape(cout, cin, k)
+        epi, outc = EPI_GATE, h
+    else:
+        rows, epi, outc = w, EPI_STORE, cout
+    tile = _pick_tile(cout)
+    packed, kc = _finish_pack(rows, k, tile)
+    b = None if bias is None else bias.detach().to(torch.float32).contiguous()
+    return PackedConv(packed, b, cin, cout, k, dilation, padding, epi, tile, kc,
+                      out_channels=outc)
+
+
+def pack_conv_transpose(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
+                        padding: int) -> PackedConv:
+    """nn.ConvTranspose1d weight [Cin, Cout, K] (K % stride == 0) as one
+    polyphase conv: GEMM row (o*u + r) holds phase r of output channel o,
+    tap j' reads x[q - (K/u - 1) + j'] with W'[(o,r)][c][j'] = W[c][o][(K/u-1-j')u + r]."""
+    w = weight.detach().to(torch.float32)
+    cin, cout, K = w.shape
+    u = stride
+    assert K % u == 0, "polyphase lowering needs kernel_size % stride == 0"
+    kp = K // u
+    # W[c][o][i*u + r] -> [c][o][i][r]
+    w4 = w.reshape(cin, cout, kp, u)
+    # rows (o, r), taps j' = kp-1-i
+    rows = w4.flip(2).permute(1, 3, 0, 2).reshape(cout * u, cin, kp)
+    tile = _pick_tile(cout * u)
+    packed, kc = _finish_pack(rows, kp, tile)
+    b = None if bias is None else bias.detach().to(torch.float32).contiguous()
+    return PackedConv(packed, b, cin, cout * u, kp, 1, kp - 1, EPI_UPSAMPLE, tile, kc,
+                      up_u=u, up_pad=padding, out_channels=cout)
+
+
+# ---------------------------------------------------------------------------
+# conv descriptor construction / launch
+# ---------------------------------------------------------------------------
+
+
+def make_out(y: torch.Tensor, *, act: int = ACT_NONE, res: Optional[torch.Tensor] = None,
+             res_scale: float = 1.0, accumulate: bool = False, post_div: float = 1.0,
+             channel_offset: int = 0) -> ConvOut:
+    o = ConvOut()
+    o.y = y.data_ptr() + 4 * channel_offset * y.stride(1)
+    o.y_bstride = y.stride(0)
+    o.y_cstride = y.stride(1)
+    o.act = act
+    if res is not None:
+        o.res = res.data_ptr() + 4 * channel_offset * res.stride(1)
+        o.res_bstride = res.stride(0)
+        o.res_cstride = res.stride(1)
+    else:
+        o.res = None
+        o.res_bstride = 0
+        o.res_cstride = 0
+    o.res_scale = res_scale
+    o.accumulate = 1 if accumulate else 0
+    o.post_div = post_div
+    return o
+
+
+def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Optional[ConvOut] = None,
+              split: Optional[int] = None, tin: Optional[int] = None, n_out: Optional[int] = None,
+              in_slope: float = 1.0, cond: Optional[torch.Tensor] = None, cond_offset: int = 0,
+              lengths: Optional[torch.Tensor] = None, t_out: int = 0,
+              x_channel_offset: int = 0) -> ConvDesc:
+    assert x.dtype == torch.float32 and x.stride(2) == 1
+    d = ConvDesc()
+    d.x = x.data_ptr() + 4 * x_channel_offset * x.stride(1)
+    d.x_bstride = x.stride(0)
+    d.x_cstride = x.stride(1)
+    d.cin = layer.cin
+    d.tin = x.shape[2] if tin is None else tin
+    d.in_slope = in_slope
+    d.w = layer.w.data_ptr()
+    d.m = layer.m
+    d.m_pad = layer.m_pad
+    d.cin_pad = layer.cin_pad
+    d.kc = layer.kc
+    d.k = layer.k
+    d.dil = layer.dil
+    d.pad_left = layer.pad_left
+    if n_out is None:
+        if layer.epi == EPI_UPSAMPLE:
+            # phases q = 0 .. Tin + ceil(pad/u) - 1 cover every t in [0, Tin*u)
+            n_out = d.tin + (layer.up_pad + layer.up_u - 1) // layer.up_u
+        else:
+            n_out = d.tin
+    d.n_out = n_out
+    d.tile = layer.tile
+    d.epi = layer.epi
+    d.bias = _ptr(layer.bias)
+    if cond is not None:
+        d.cond = cond.data_ptr() + 4 * cond_offset
+        d.cond_bstride = cond.stride(0)
+    else:
+        d.cond = None
+        d.cond_bstride = 0
+    d.split = layer.m if split is None else split
+    d.up_u = layer.up_u
+    d.up_pad = layer.up_pad
+    d.t_out = t_out
+    d.lengths = _ptr(lengths)
+    d.out0 = out0
+    if out1 is not None:
+        d.out1 = out1
+    return d
+
+
+def conv1d_launch(desc: ConvDesc, batch: int, device: torch.device):
+    lib = _lib.load()
+    check(lib.vits_conv1d_forward(C.byref(desc), batch, _stream_ptr(device)), "vits_conv1d_forward")
+
+
+def conv1d_launch_seq(descs, batch: int, device: torch.device):
+    lib = _lib.load()
+    arr = (ConvDesc * len(descs))(*descs)
+    check(lib.vits_conv1d_forward_seq(arr, len(descs), batch, _stream_ptr(device)),
+          "vits_conv1d_forward_seq")
+
+
+def conv1d(x: torch.Tensor, layer: PackedConv, *, in_slope: float = 1.0, act: int = ACT_NONE,
+           cond: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+           res_scale: float = 1.0, lengths: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, accumulate: bool = False,
+           post_div: float = 1.0, t_out: Optional[int] = None) -> torch.Tensor:
+    """Run one packed conv on [B, cin, T] fp32 (device) and return [B, out_channels, T_out]."""
+    require_device(x, cond, residual, lengths)
+    x = x.contiguous() if x.stride(2) != 1 else x
+    B, _, T = x.shape
+    if layer.epi == EPI_UPSAMPLE:
+        T_out = T * layer.up_u if t_out is None else t_out
+    else:
+        T_out = T
+    if out is None:
+        out = torch.empty(B, layer.out_channels, T_out, device=x.device, dtype=torch.float32)
+    o0 = make_out(out, act=act, res=residual, res_scale=res_scale, accumulate=accumulate,
+                  post_div=post_div)
+    if lengths is not None:
+        lengths = lengths.to(device=x.device, dtype=torch.int32).contiguous()
+    d = make_desc(layer, x, o0, in_slope=in_slope, cond=cond, lengths=lengths, t_out=T_out)
+    conv1d_launch(d, B, x.device)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# small kernels
+# ---------------------------------------------------------------------------
+
+
+def linear_rows(g: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y[b] = weight @ g[b] + bias (per-utterance conditioning)."""
+    require_device(g, weight, bias)
+    g = g.contiguous().float()
+    B, n_in = g.shape
+    n_out = weight.shape[0]
+    if out is None:
+        out = torch.empty(B, n_out, device=g.device, dtype=torch.float32)
+    lib = _lib.load()
+    check(lib.vits_linear_forward(g.data_ptr(), g.stride(0), weight.data_ptr(), _ptr(bias),
+                                  out.data_ptr(), out.stride(0), B, n_out, n_in,
+                                  _stream_ptr(g.device)), "vits_linear_forward")
+    return out
+
+
+def expand_prior(attn: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor, noise: torch.Tensor,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    require_device(attn, m_p, s_p, noise)
+    attn = attn.contiguous().float()
+    m_p = m_p.contiguous().float()
+    s_p = s_p.contiguous().float()
+    noise = noise.contiguous().float()
+    B, Ty, Tx = attn.shape
+    Cc = m_p.shape[1]
+    if out is None:
+        out = torch.empty(B, Cc, Ty, device=attn.device, dtype=torch.float32)
+    lib = _lib.load()
+    check(lib.vits_expand_prior(attn.data_ptr(), m_p.data_ptr(), s_p.data_ptr(), noise.data_ptr(),
+                                out.data_ptr(), B, Cc, Ty, Tx, _stream_ptr(attn.device)),
+          "vits_expand_prior")
+    return out
+
+
+def conv_post_tanh(x: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Tensor] = None):
+    require_device(x, weight)
+    B, Cc, T = x.shape
+    k = weight.shape[-1]
+    w = weight.reshape(Cc, k).contiguous().float()
+    if out is None:
+        out = torch.empty(B, 1, T, device=x.device, dtype=torch.float32)
+    lib = _lib.load()
+    check(lib.vits_conv_post_tanh(x.data_ptr(), x.stride(0), x.stride(1), w.data_ptr(),
+                                  out.data_ptr(), B, Cc, T, k, _stream_ptr(x.device)),
+          "vits_conv_post_tanh")
+    return out
+
+
+def layer_norm_channels(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor],
+                        eps: float = 1e-5, residual: Optional[torch.Tensor] = None,
+                        out: Optional[torch.Tensor] = None,
+                        lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
+    require_device(x, residual)
+    x = x.contiguous()
+    B, Cc, T = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    lib = _lib.load()
+    check(lib.vits_layer_norm_channels(x.data_ptr(), _ptr(residual), _ptr(gamma), _ptr(beta),
+                                       out.data_ptr(), B, Cc, T, eps, _ptr(lengths),
+                                       _stream_ptr(x.device)), "vits_layer_norm_channels")
+    return out
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, n_heads: int,
+              lengths: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
+    """softmax((q/sqrt(d)) k^T, masked -1e4) v on [B, H*D, T] channel-major tensors."""
+    require_device(q, k, v, lengths)
+    B, Cc, T = q.shape
+    D = Cc // n_heads
+    assert q.stride() == k.stride() == v.stride() and q.stride(2) == 1 and q.stride(1) == T
+    if out is None:
+        out = torch.empty(B, Cc, T, device=q.device, dtype=torch.float32)
+    assert out.stride() == q.stride()
+    lib = _lib.load()
+    check(lib.vits_attention_forward(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B,
+                                     n_heads, D, T, q.stride(0), _ptr(lengths),
+                                     _stream_ptr(q.device)), "vits_attention_forward")
+    return out
+
+
+_DT = {torch.float32: _lib.DT_F32, torch.float16: _lib.DT_F16, torch.bfloat16: _lib.DT_BF16,
+       torch.int32: _lib.DT_I32}
+
+
+def maximum_path(neg_cent: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """monotonic_align.maximum_path on the GPU (models.py:498 call contract)."""
+    require_device(neg_cent, mask)
+    dtype = neg_cent.dtype
+    if dtype not in _DT:
+        raise _lib.VitsAmdError(f"maximum_path: unsupported dtype {dtype}")
+    nc = neg_cent.detach().to(torch.float32).contiguous()
+    mk = mask.detach()
+    if mk.dtype not in _DT:
+        mk = mk.to(torch.float32)
+    mk = mk.contiguous()
+    B, Tt, Ts = nc.shape
+    if mk.shape != nc.shape:
+        raise _lib.VitsAmdError(f"maximum_path: mask {tuple(mk.shape)} vs neg_cent {tuple(nc.shape)}")
+    path = torch.empty(B, Tt, Ts, device=nc.device, dtype=dtype)
+    lib = _lib.load()
+    wsb = int(lib.vits_maximum_path_workspace(B, Tt, Ts))
+    ws = torch.empty(max(wsb, 16), device=nc.device, dtype=torch.uint8)
+    check(lib.vits_maximum_path(nc.data_ptr(), mk.data_ptr(), _DT[mk.dtype], path.data_ptr(),
+                                _DT[dtype], B, Tt, Ts, ws.data_ptr(), ws.numel(),
+                                _stream_ptr(nc.device)), "vits_maximum_path")
+    return path
+
+
+def maximum_path_lengths(neg_cent: torch.Tensor, t_t: torch.Tensor, t_s: torch.Tensor,
+                         dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    require_device(neg_cent, t_t, t_s)
+    nc = neg_cent.detach().to(torch.float32).contiguous()
+    B, Tt, Ts = nc.shape
+    tt = t_t.to(torch.int32).contiguous()
+    ts = t_s.to(torch.int32).contiguous()
+    path = torch.empty(B, Tt, Ts, device=nc.device, dtype=dtype)
+    lib = _lib.load()
+    wsb = int(lib.vits_maximum_path_workspace(B, Tt, Ts))
+    ws = torch.empty(max(wsb, 16), device=nc.device, dtype=torch.uint8)
+    check(lib.vits_maximum_path_lengths(nc.data_ptr(), tt.data_ptr(), ts.data_ptr(),
+                                        path.data_ptr(), _DT[dtype], B, Tt, Ts, ws.data_ptr(),
+                                        ws.numel(), _stream_ptr(nc.device)),
+          "vits_maximum_path_lengths")
+    return path
+
+
+# ---------------------------------------------------------------------------
+# STFT magnitude with autograd
+# ---------------------------------------------------------------------------
+
+
+class _StftMag(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, window, n_fft, hop, win, pad, eps):
+        require_device(x, window)
+        x = x.contiguous().float()
+        window = window.contiguous().float()
+        B, L = x.shape
+        frames = (L + 2 * pad - n_fft) // hop + 1
+        nb = n_fft // 2 + 1
+        mag = torch.empty(B, nb, frames, device=x.device, dtype=torch.float32)
+        need_grad = ctx.needs_input_grad[0]
+        re = torch.empty_like(mag) if need_grad else None
+        im = torch.empty_like(mag) if need_grad else None
+        lib = _lib.load()
+        check(lib.vits_stft_mag_forward(x.data_ptr(), B, L, window.data_ptr(), n_fft, hop, win, pad,
+                                        eps, mag.data_ptr(), _ptr(re), _ptr(im),
+                                        _stream_ptr(x.device)), "vits_stft_mag_forward")
+        if need_grad:
+            ctx.save_for_backward(mag, re, im, window)
+        ctx.cfg = (B, L, n_fft, hop, win, pad)
+        return mag
+
+    @staticmethod
+    def backward(ctx, gmag):
+        mag, re, im, window = ctx.saved_tensors
+        B, L, n_fft, hop, win, pad = ctx.cfg
+        gmag = gmag.contiguous().float()
+        gx = torch.empty(B, L, device=gmag.device, dtype=torch.float32)
+        lib = _lib.load()
+        nws = int(lib.vits_stft_workspace(B, L, n_fft, hop, pad))
+        ws = torch.empty(max(nws, 1), device=gmag.device, dtype=torch.float32)
+        check(lib.vits_stft_mag_backward(gmag.data_ptr(), mag.data_ptr(), re.data_ptr(),
+                                         im.data_ptr(), window.data_ptr(), B, L, n_fft, hop, win,
+                                         pad, gx.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         _stream_ptr(gmag.device)), "vits_stft_mag_backward")
+        return gx, None, None, None, None, None, None
+
+
+def stft_mag(x: torch.Tensor, window: torch.Tensor, n_fft: int, hop: int, win: int,
+             pad: Optional[int] = None, eps: float = 1e-7) -> torch.Tensor:
+    """sqrt(|STFT(x)|^2 + eps), [B, n_fft//2+1, frames]; differentiable in x."""
+    if pad is None:
+        pad = n_fft // 2
+    out = _StftMag.apply(x, window, n_fft, hop, win, pad, eps)
+    return out
