@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X VITS hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): ``SynthesizerTrn.infer_p2`` — prior
+expansion + reverse flow + HiFi-GAN decoder — at batch 16, Tx=100 tokens,
+5 frames/token -> Ty=500 frames -> 96,000 output samples per utterance
+(configs/base.json: 16 kHz, hop 192), fp32, random-init weights
+(deterministic key-hash fill), synthetic inputs.  One step = one infer_p2
+call on one batch with every input already resident in HBM.
+
+Multi-GPU: inference does not shard: N ranks run N
+independent replicas of the same step; value = all output samples / the
+slowest rank's time ("scaling": "weak").
+
+Extra fields:
+  roofline      the dominant kernel (conv1d_mfma_kernel, every conv launch of
+                the step): algorithmic FLOPs / HIP-event-timed kernel time,
+                against the fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
+  cpu_baseline  the CPU oracle (oracle/vits_oracle.py, torch fp32 CPU: the
+                reference algorithm restated) on a bounded sample.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+       [--tx 100] [--ty 500] [--graph] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "22.05 kHz audio samples/sec/GPU (infer RTF) + train utt/sec at 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3
+HOP = 192
+SR = 16000
+
+BASE_MODEL = dict(inter_channels=192, hidden_channels=256, filter_channels=512, n_heads=2,
+                  n_layers=6, kernel_size=5, p_dropout=0.1, ffn="FFN2", resblock="2",
+                  resblock_kernel_sizes=[3, 7, 11],
+                  resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+                  upsample_rates=[8, 6, 2, 2], upsample_initial_channel=512,
+                  upsample_kernel_sizes=[16, 12, 4, 4], kernel_size_q=5, n_layers_q=16,
+                  hidden_size_d=256, kernel_size_d=5, p_dropout_d=0.5, act_func_d="ReLU",
+                  act_func_params_d={}, use_spectral_norm=False, dilation_rate=[1, 1, 1, 1],
+                  n_flows=4, gin_channels=1024)
+
+
+def build_model(device):
+    from vits_amd.models import SynthesizerTrn
+    from vits_amd.utils import deterministic_fill_
+
+    m = SynthesizerTrn(256, 513, 48, n_speakers=2048, **BASE_MODEL).eval()
+    deterministic_fill_(m)
+    return m.to(device)
+
+
+def make_inputs(B, Tx, Ty, device, seed=1234):
+    from vits_amd.commons import infer_path
+
+    g = torch.Generator().manual_seed(seed)
+    per = Ty // Tx
+    dur = torch.full((1, 1, Tx), float(per))
+    dur[0, 0, -1] += Ty - per * Tx
+    attn = infer_path(dur, Tx, Ty).expand(B, Ty, Tx).contiguous()
+    m_p = torch.randn(B, 192, Tx, generator=g)
+    s_p = torch.rand(B, 192, Tx, generator=g) + 0.3
+    gg = torch.randn(B, 1024, generator=g) * 0.5
+    noise = torch.randn(B, 192, Ty, generator=g) * 0.707
+    return [t.to(device) for t in (attn, m_p, s_p, gg, noise)]
+
+
+def cpu_baseline(model, Tx, Ty, budget_s=12.0):
+    """Oracle (torch CPU fp32) infer_p2 on B=1 utterances until ~budget_s."""
+    from oracle import vits_oracle as V
+
+    sd = V.SD({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    attn, m_p, s_p, g, noise = make_inputs(1, Tx, Ty, "cpu")
+    cores = torch.get_num_threads()
+    with torch.no_grad():
+        V.infer_p2(sd, attn, m_p, s_p, g, noise, BASE_MODEL)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            V.infer_p2(sd, attn, m_p, s_p, g, noise, BASE_MODEL)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or n >= 50:
+                break
+    samples = n * Ty * HOP
+    return {"value": samples / el, "unit": "output samples/s", "cores": cores, "kind": "port",
+            "sample": f"{n} x infer_p2 B=1 Tx={Tx} Ty={Ty} ({Ty * HOP} samples each) in {el:.1f} s, "
+                      f"oracle/vits_oracle.py torch-CPU fp32, torch.set_num_threads({cores})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--tx", type=int, default=100)
+    ap.add_argument("--ty", type=int, default=500)
+    ap.add_argument("--graph", action="store_true", help="replay a captured hipGraph per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank)
+    device = torch.device("cuda", local_rank)
+
+    model = build_model(device)
+    B, Tx, Ty = args.batch, args.tx, args.ty
+    inputs = make_inputs(B, Tx, Ty, device, seed=1234 + rank)
+
+    step = None
+    if args.graph:
+        run = model.capture_infer_p2(B, Tx, Ty)
+        step = lambda: run(*inputs)  # noqa: E731
+    else:
+        step = lambda: model.infer_p2(*inputs)  # noqa: E731
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+
+        roof = None
+        if not args.no_roofline and not args.graph:
+            from vits_amd.ops import ConvTimer
+
+            with ConvTimer() as timer:
+                for _ in range(args.steps):
+                    model.infer_p2(*inputs)
+            s = timer.summary()
+            per_launch_flops = s["total_flops"] / max(1, s["launches"])
+            achieved = (s["total_flops"] / 1e12) / (s["total_ms"] / 1e3)
+            roof = {"bound": "mfma", "kernel": "conv1d_mfma_kernel (all conv launches of a step)",
+                    "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": None, "launches_per_step": s["launches"] // args.steps,
+                    "avg_launch_ms": round(s["avg_ms"], 4),
+                    "flops_per_launch": int(per_launch_flops),
+                    "conv_ms_per_step": round(s["total_ms"] / args.steps, 3)}
+
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    samples_per_rank = args.steps * B * Ty * HOP
+    total_samples = samples_per_rank * world
+    value = total_samples / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "output samples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic: random-init weights (deterministic key-hash fill), random priors, "
+                    "5 frames/token durations",
+            "config": {"workload": f"SynthesizerTrn.infer_p2 batch={B} Tx={Tx} Ty={Ty} "
+                                   f"(configs/base.json, 16 kHz, hop 192) per GPU",
+                       "global_batch": B * world, "seq_len": Ty,
+                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
+                       "graph": bool(args.graph)},
+            "rtf_16k": round((ms_per_step / 1e3) / (B * Ty * HOP / SR), 6),
+            "x_realtime_22k": round(value / world / 22050.0, 1),
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(model, Tx, Ty)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

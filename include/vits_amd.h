@@ -60,6 +60,7 @@ extern "C" {
 #define VITS_ACT_NONE 0
 #define VITS_ACT_RELU 1
 #define VITS_ACT_TANH 2
+#define VITS_ACT_EXP 3
 
 /* tile configurations (rows x cols of one workgroup) */
 #define VITS_TILE_128x128 0
@@ -80,10 +81,13 @@ typedef struct vits_conv_out {
 } vits_conv_out;
 
 typedef struct vits_conv1d_desc {
-  /* input x: [B][cin][*], element (b, c, t) at b*x_bstride + c*x_cstride + t */
+  /* input x: element (b, c, t) at b*x_bstride + c*x_cstride + t*x_tstride   */
+  /* ([B][C][T] activations: x_tstride = 1; time-major [B][T][C]: x_cstride */
+  /* = 1, x_tstride = C, used for the text-embedding Linear)                */
   const float* x;
   int64_t x_bstride;
   int32_t x_cstride;
+  int32_t x_tstride;
   int32_t cin;
   int32_t tin;            /* valid input positions; outside reads as 0        */
   float in_slope;         /* prologue leaky-relu slope on x; 1.0 = identity   */
@@ -129,7 +133,10 @@ int vits_linear_forward(const float* g, int64_t g_bstride, const float* w, const
 /*                    + noise[b][c][t] * sum_x attn[b][t][x] s[b][c][x]   */
 /* ---------------------------------------------------------------------- */
 int vits_expand_prior(const float* attn, const float* m, const float* s, const float* noise,
-                      float* z, int batch, int channels, int t_y, int t_x, void* stream);
+                      float* z, int batch, int channels, int t_y, int t_x, int exp_s,
+                      float noise_scale, void* stream);
+/* exp_s = 0: z = A.m + noise * (A.s)                 (infer_p2, models.py:569-571) */
+/* exp_s = 1: z = A.m + noise * exp(A.s) * noise_scale  (inference, models.py:529-532) */
 
 /* ---------------------------------------------------------------------- */
 /* Generator tail: y[b][t] = tanh(sum_{c,j} w[c][j] lrelu(x[b][c][t-3+j], 0.01)) */
@@ -185,20 +192,28 @@ int vits_stft_mag_backward(const float* grad_mag, const float* mag, const float*
 int64_t vits_stft_workspace(int batch, int length, int n_fft, int hop, int pad);
 
 /* ---------------------------------------------------------------------- */
-/* channel LayerNorm over dim 1 of [B][C][T] (+ optional residual input)  */
-/* y = LN(x + r) * gamma + beta; eps as given                             */
+/* channel LayerNorm over dim 1 of [B][C][T]:                             */
+/*   v = LN(x + r) * gamma + beta                (r, gamma, beta optional) */
+/*   v = (v + post_add[b][c]) * scale + pos[t][c] * (*pos_alpha)           */
+/*   y = (t < lengths[b]) ? v : 0                (lengths optional)        */
+/* post_add / pos / pos_alpha optional (NULL); pos is [T][C] (sin table);  */
+/* pos_alpha is a device scalar (the learnable TextEncoder.alpha).        */
 /* ---------------------------------------------------------------------- */
 int vits_layer_norm_channels(const float* x, const float* r, const float* gamma,
                              const float* beta, float* y, int batch, int channels, int t_len,
-                             float eps, const int32_t* lengths, void* stream);
+                             float eps, const int32_t* lengths, const float* post_add,
+                             int64_t post_add_bstride, float scale, const float* pos,
+                             const float* pos_alpha, void* stream);
 
 /* ---------------------------------------------------------------------- */
-/* scaled-dot-product attention over [B][H*D][T] channel-major q/k/v,     */
-/* key mask from lengths (fill -1e4), out [B][H*D][T]                      */
+/* scaled-dot-product attention over [B][H*D][T] channel-major q/k/v      */
+/* (batch stride qkv_bstride, e.g. slices of one fused q|k|v buffer), key */
+/* mask from lengths (fill -1e4), out [B][H*D][T] with out_bstride         */
 /* ---------------------------------------------------------------------- */
 int vits_attention_forward(const float* q, const float* k, const float* v, float* out,
                            int batch, int heads, int head_dim, int t_len,
-                           int64_t bstride, const int32_t* lengths, void* stream);
+                           int64_t qkv_bstride, int64_t out_bstride, const int32_t* lengths,
+                           void* stream);
 
 /* library introspection */
 const char* vits_amd_version(void);

@@ -1,0 +1,62 @@
+"""The C-ABI library loads on a GPU-less host and exports every entry point
+include/vits_amd.h declares (no compute calls here)."""
+import ctypes
+import os
+import re
+
+from common import HERE
+
+ROOT = os.path.dirname(HERE)
+
+
+def _declared():
+    with open(os.path.join(ROOT, "include", "vits_amd.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(vits_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "vits_conv1d_forward" in names and "vits_maximum_path" in names
+    assert len(names) >= 15
+
+
+def test_library_exports_every_declared_symbol():
+    from vits_amd import _lib
+
+    lib = _lib.load()
+    raw = ctypes.CDLL(_lib.lib_path())
+    missing = [n for n in _declared() if not hasattr(raw, n)]
+    assert not missing, missing
+    # the Python binding covers every declared symbol too
+    assert sorted(_lib.EXPORTED_SYMBOLS) == _declared()
+    assert lib.vits_amd_version().startswith(b"vits_amd")
+
+
+def test_struct_layout_matches_header():
+    """ctypes struct sizes equal the C sizeof (checked by compiling a probe)."""
+    import subprocess
+    import tempfile
+
+    from vits_amd._lib import ConvDesc, ConvOut
+
+    probe = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "vits_amd.h"
+int main(){printf("%zu %zu %zu %zu\n", sizeof(vits_conv1d_desc), sizeof(vits_conv_out),
+ offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths)); return 0;}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "p.c")
+        exe = os.path.join(d, "p")
+        with open(src, "w") as f:
+            f.write(probe)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    assert int(out[0]) == ctypes.sizeof(ConvDesc)
+    assert int(out[1]) == ctypes.sizeof(ConvOut)
+    assert int(out[2]) == ConvDesc.out0.offset
+    assert int(out[3]) == ConvDesc.lengths.offset

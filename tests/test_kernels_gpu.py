@@ -229,3 +229,22 @@ def test_attention(device, T, lens):
     ref = torch.matmul(F.softmax(sc, -1), vh).transpose(2, 3).reshape(B, H * D, T)
     out = ops.attention(q.to(device), k.to(device), v.to(device), H, lengths=lengths.to(device))
     _close(out, ref, tol=2e-5, what="attention")
+
+
+def test_attention_fused_qkv_strides(device):
+    """q|k|v as channel slices of one [B, 3C, T] projection buffer (the
+    engine's layout): batch stride 3*C*T for inputs, C*T for the output."""
+    from vits_amd import engine
+
+    g = torch.Generator().manual_seed(12)
+    B, H, D, T = 3, 2, 128, 45
+    qkv = torch.randn(B, 3 * H * D, T, generator=g)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    qh = q.reshape(B, H, D, T).transpose(2, 3)
+    kh = k.reshape(B, H, D, T).transpose(2, 3)
+    vh = v.reshape(B, H, D, T).transpose(2, 3)
+    ref = torch.matmul(F.softmax(torch.matmul(qh / D ** 0.5, kh.transpose(-2, -1)), -1), vh)
+    ref = ref.transpose(2, 3).reshape(B, H * D, T)
+    out = torch.empty(B, H * D, T, device=device)
+    engine._attention_into(qkv.to(device), H * D, H, None, out)
+    _close(out, ref, tol=2e-5, what="fused-qkv attention")

@@ -20,7 +20,7 @@ VITS_E_SHAPE = -2
 VITS_E_UNSUP = -3
 
 EPI_STORE, EPI_GATE, EPI_UPSAMPLE = 0, 1, 2
-ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_TANH, ACT_EXP = 0, 1, 2, 3
 TILE_128x128, TILE_64x256, TILE_32x256 = 0, 1, 2
 TILE_ROWS = {TILE_128x128: 128, TILE_64x256: 64, TILE_32x256: 32}
 DT_F32, DT_F16, DT_BF16, DT_I32 = 0, 1, 2, 3
@@ -46,6 +46,7 @@ class ConvDesc(C.Structure):
         ("x", C.c_void_p),
         ("x_bstride", C.c_int64),
         ("x_cstride", C.c_int32),
+        ("x_tstride", C.c_int32),
         ("cin", C.c_int32),
         ("tin", C.c_int32),
         ("in_slope", C.c_float),
@@ -83,7 +84,7 @@ _SIGS = {
     ),
     "vits_expand_prior": (
         C.c_int,
-        [C.c_void_p] * 5 + [C.c_int] * 4 + [C.c_void_p],
+        [C.c_void_p] * 5 + [C.c_int] * 5 + [C.c_float, C.c_void_p],
     ),
     "vits_conv_post_tanh": (
         C.c_int,
@@ -115,11 +116,13 @@ _SIGS = {
     "vits_stft_workspace": (C.c_int64, [C.c_int] * 5),
     "vits_layer_norm_channels": (
         C.c_int,
-        [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_float, C.c_void_p, C.c_void_p],
+        [C.c_void_p] * 5 + [C.c_int] * 3
+        + [C.c_float, C.c_void_p, C.c_void_p, C.c_int64, C.c_float, C.c_void_p, C.c_void_p,
+           C.c_void_p],
     ),
     "vits_attention_forward": (
         C.c_int,
-        [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_int64, C.c_void_p, C.c_void_p],
+        [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p],
     ),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ k,
                                                       const float* __restrict__ v,
                                                       float* __restrict__ out, int H, int T,
-                                                      int64_t bstride,
+                                                      int64_t bstride, int64_t out_bstride,
                                                       const int32_t* __restrict__ lengths) {
   static_assert(D % 32 == 0, "head dim multiple of 32");
   constexpr int KS = D / 2;   // k-steps of the QK product
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const float* __restrict__ 
   // epilogue: O^T rows = d, cols = query (this lane)
   if (!qvalid) return;
   const float inv = 1.0f / l_run;
-  float* ob = out + hoff;
+  float* ob = out + (int64_t)b * out_bstride + (int64_t)h * D * T;
 #pragma unroll
   for (int t = 0; t < DT; ++t)
 #pragma unroll
@@ -133,23 +133,25 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const float* __restrict__ 
 
 extern "C" int vits_attention_forward(const float* q, const float* k, const float* v, float* out,
                                       int batch, int heads, int head_dim, int t_len,
-                                      int64_t bstride, const int32_t* lengths, void* stream) {
+                                      int64_t bstride, int64_t out_bstride,
+                                      const int32_t* lengths, void* stream) {
   VITS_CHECK_ARG(q && k && v && out && batch > 0 && heads > 0 && t_len > 0);
   VITS_CHECK_SHAPE(bstride >= (int64_t)heads * head_dim * t_len);
+  VITS_CHECK_SHAPE(out_bstride >= (int64_t)heads * head_dim * t_len);
   dim3 grid((t_len + AT_Q - 1) / AT_Q, heads, batch);
   hipStream_t s = as_stream(stream);
   switch (head_dim) {
     case 64:
       hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(64), 0, s, q, k, v, out, heads, t_len,
-                         bstride, lengths);
+                         bstride, out_bstride, lengths);
       break;
     case 128:
       hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(64), 0, s, q, k, v, out, heads, t_len,
-                         bstride, lengths);
+                         bstride, out_bstride, lengths);
       break;
     case 96:
       hipLaunchKernelGGL(attn_fwd_kernel<96>, grid, dim3(64), 0, s, q, k, v, out, heads, t_len,
-                         bstride, lengths);
+                         bstride, out_bstride, lengths);
       break;
     default:
       return VITS_E_UNSUP;

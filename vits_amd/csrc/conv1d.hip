@@ -41,6 +41,7 @@ struct OutDesc {
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == VITS_ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == VITS_ACT_TANH) return tanhf(v);
+  if (act == VITS_ACT_EXP) return expf(v);
   return v;
 }
 
@@ -94,6 +95,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const float* xb = p.x + (int64_t)b * p.x_bstride;
+  const int64_t xts = p.x_tstride;
   const int xstart = n0 - p.pad_left;
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc
         const int tt = xstart + t;
         float v = 0.f;
         if (crow && t < xw && tt >= 0 && tt < p.tin) {
-          v = xr[tt];
+          v = xr[tt * xts];
           if (act_in) v = v < 0.f ? v * slope : v;
         }
         xs[c * xw_pad + t] = v;
@@ -253,7 +255,8 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   VITS_CHECK_ARG(batch > 0 && d.cin > 0 && d.m > 0 && d.k > 0 && d.dil > 0 && d.n_out > 0);
   VITS_CHECK_SHAPE(d.kc >= 2 && (d.kc % 2) == 0 && d.cin_pad % d.kc == 0 && d.cin_pad >= d.cin);
   VITS_CHECK_SHAPE(d.m_pad % 128 == 0 && d.m_pad >= d.m);
-  VITS_CHECK_SHAPE(d.x_cstride >= d.tin && d.tin >= 0);
+  VITS_CHECK_SHAPE(d.tin >= 0 && d.x_tstride >= 1);
+  VITS_CHECK_SHAPE(d.x_tstride != 1 || d.x_cstride >= d.tin);
   if (d.epi == VITS_EPI_GATE) VITS_CHECK_SHAPE((d.m % 2) == 0);
   if (d.epi == VITS_EPI_UPSAMPLE) VITS_CHECK_SHAPE(d.up_u > 0 && d.m % d.up_u == 0 && d.t_out > 0);
   if (d.epi == VITS_EPI_STORE && d.split < d.m) VITS_CHECK_ARG(d.out1.y != nullptr);

@@ -17,7 +17,11 @@ __global__ __launch_bounds__(256) void ln_channels_kernel(const float* x,
                                                           const float* __restrict__ beta,
                                                           float* y, int C, int T,
                                                           float eps,
-                                                          const int32_t* __restrict__ lengths) {
+                                                          const int32_t* __restrict__ lengths,
+                                                          const float* __restrict__ post_add,
+                                                          int64_t post_add_bstride, float scale,
+                                                          const float* __restrict__ pos,
+                                                          const float* __restrict__ pos_alpha) {
   __shared__ float part[4][64];
   __shared__ float stat[2][64];
   const int b = blockIdx.y;
@@ -58,11 +62,17 @@ __global__ __launch_bounds__(256) void ln_channels_kernel(const float* x,
   const float rstd = stat[1][lane];
   if (!valid) return;
   const bool zero = lengths && t >= lengths[b];
+  const float* pa = post_add ? post_add + (int64_t)b * post_add_bstride : nullptr;
+  const float alpha = pos ? *pos_alpha : 0.f;
   for (int c = c0; c < c1; ++c) {
     const int64_t o = base + (int64_t)c * T + t;
     const float xv = r ? x[o] + r[o] : x[o];
     float out = (xv - mean) * rstd;
-    out = out * (gamma ? gamma[c] : 1.f) + (beta ? beta[c] : 0.f);
+    if (gamma) out = out * gamma[c];
+    if (beta) out = out + beta[c];
+    if (pa) out = out + pa[c];
+    if (scale != 1.0f) out = out * scale;
+    if (pos) out = out + pos[(int64_t)t * C + c] * alpha;
     y[o] = zero ? 0.f : out;
   }
 }
@@ -72,10 +82,14 @@ __global__ __launch_bounds__(256) void ln_channels_kernel(const float* x,
 extern "C" int vits_layer_norm_channels(const float* x, const float* r, const float* gamma,
                                         const float* beta, float* y, int batch, int channels,
                                         int t_len, float eps, const int32_t* lengths,
+                                        const float* post_add, int64_t post_add_bstride,
+                                        float scale, const float* pos, const float* pos_alpha,
                                         void* stream) {
   VITS_CHECK_ARG(x && y && batch > 0 && channels > 0 && t_len > 0);
+  VITS_CHECK_ARG(!pos || pos_alpha);
   dim3 grid((t_len + 63) / 64, batch);
   hipLaunchKernelGGL(ln_channels_kernel, grid, dim3(256), 0, as_stream(stream), x, r, gamma, beta,
-                     y, channels, t_len, eps, lengths);
+                     y, channels, t_len, eps, lengths, post_add, post_add_bstride, scale, pos,
+                     pos_alpha);
   return vits_launch_status();
 }

@@ -60,7 +60,8 @@ __global__ __launch_bounds__(256) void expand_prior_kernel(const float* __restri
                                                            const float* __restrict__ s,
                                                            const float* __restrict__ noise,
                                                            float* __restrict__ z, int channels,
-                                                           int t_y, int t_x) {
+                                                           int t_y, int t_x, int exp_s,
+                                                           float noise_scale) {
   extern __shared__ float tile[];  // [2][channels][EP_T+1]
   float* tm = tile;
   float* ts = tile + channels * (EP_T + 1);
@@ -115,7 +116,9 @@ __global__ __launch_bounds__(256) void expand_prior_kernel(const float* __restri
     const int t = t0 + tl;
     if (t < t_y) {
       const int64_t o = ((int64_t)b * channels + c) * t_y + t;
-      z[o] = tm[c * (EP_T + 1) + tl] + noise[o] * ts[c * (EP_T + 1) + tl];
+      const float sv = ts[c * (EP_T + 1) + tl];
+      z[o] = exp_s ? tm[c * (EP_T + 1) + tl] + noise[o] * expf(sv) * noise_scale
+                   : tm[c * (EP_T + 1) + tl] + noise[o] * sv;
     }
   }
 }
@@ -182,13 +185,13 @@ extern "C" int vits_linear_forward(const float* g, int64_t g_bstride, const floa
 
 extern "C" int vits_expand_prior(const float* attn, const float* m, const float* s,
                                  const float* noise, float* z, int batch, int channels, int t_y,
-                                 int t_x, void* stream) {
+                                 int t_x, int exp_s, float noise_scale, void* stream) {
   VITS_CHECK_ARG(attn && m && s && noise && z && batch > 0 && channels > 0 && t_y > 0 && t_x > 0);
   VITS_CHECK_SHAPE(channels <= 256);
   const size_t lds = sizeof(float) * 2 * channels * (EP_T + 1);
   dim3 grid((t_y + EP_T - 1) / EP_T, batch);
   hipLaunchKernelGGL(expand_prior_kernel, grid, dim3(256), lds, as_stream(stream), attn, m, s,
-                     noise, z, channels, t_y, t_x);
+                     noise, z, channels, t_y, t_x, exp_s, noise_scale);
   return vits_launch_status();
 }
 

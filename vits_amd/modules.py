@@ -1,0 +1,215 @@
+"""Building blocks of the VITS generator (reference ``modules.py``).
+
+Parameter names and shapes are the reference's (legacy weight-norm
+``weight_g``/``weight_v``), so reference checkpoints load unchanged.
+
+Two execution modes per block:
+* ``forward`` — the training path: PyTorch-ROCm ops under autograd (the
+  fused HIP kernels are forward-only; backward kernels are a §8(f) "next"
+  item).  Semantics follow the cited reference lines exactly.
+* ``infer`` — the inference path: lowered to libvits_amd kernels through
+  ``vits_amd.engine`` (see there); no torch compute op runs.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+from torch.nn.utils import weight_norm, remove_weight_norm  # noqa: F401  (legacy names)
+
+from .commons import get_padding, init_weights
+
+LRELU_SLOPE = 0.1
+
+
+class LayerNorm(nn.Module):
+    """Channel LayerNorm on [B, C, T] (modules.py:33-44)."""
+
+    def __init__(self, channels, eps=1e-5):
+        super().__init__()
+        self.channels = channels
+        self.eps = eps
+        self.gamma = nn.Parameter(torch.ones(channels))
+        self.beta = nn.Parameter(torch.zeros(channels))
+
+    def forward(self, x):
+        y = F.layer_norm(x.transpose(1, -1), (self.channels,), self.gamma, self.beta, self.eps)
+        return y.transpose(1, -1)
+
+
+class WN(nn.Module):
+    """Gated dilated-conv stack (modules.py:93-182)."""
+
+    def __init__(self, hidden_channels, kernel_size, dilation_rate, n_layers, gin_channels=0,
+                 p_dropout=0):
+        super().__init__()
+        assert kernel_size % 2 == 1
+        self.hidden_channels = hidden_channels
+        self.kernel_size = (kernel_size,)
+        self.dilation_rate = dilation_rate
+        self.n_layers = n_layers
+        self.gin_channels = gin_channels
+        self.p_dropout = p_dropout
+        self.in_layers = nn.ModuleList()
+        self.res_skip_layers = nn.ModuleList()
+        self.drop = nn.Dropout(p_dropout)
+        if gin_channels != 0:
+            self.cond_layer = weight_norm(nn.Linear(gin_channels, 2 * hidden_channels * n_layers))
+        for i in range(n_layers):
+            dilation = dilation_rate ** i
+            padding = int((kernel_size * dilation - dilation) / 2)
+            self.in_layers.append(weight_norm(
+                nn.Conv1d(hidden_channels, 2 * hidden_channels, kernel_size, dilation=dilation,
+                          padding=padding)))
+            rs = 2 * hidden_channels if i < n_layers - 1 else hidden_channels
+            self.res_skip_layers.append(weight_norm(nn.Conv1d(hidden_channels, rs, 1)))
+
+    def _gate(self, x_in, g, i):
+        H = self.hidden_channels
+        if g is not None:
+            x_in = x_in + g[:, i * 2 * H:(i + 1) * 2 * H].unsqueeze(-1)
+        return torch.tanh(x_in[:, :H]) * torch.sigmoid(x_in[:, H:])
+
+    def forward(self, x, x_mask, g=None, **kwargs):
+        H = self.hidden_channels
+        output = torch.zeros_like(x)
+        if self.gin_channels != 0:
+            g = self.cond_layer(g)
+        for i in range(self.n_layers):
+            acts = self.drop(self._gate(self.in_layers[i](x), g if self.gin_channels else None, i))
+            rs = self.res_skip_layers[i](acts)
+            if i < self.n_layers - 1:
+                x = (x + rs[:, :H]) * x_mask
+                output = output + rs[:, H:]
+            else:
+                output = output + rs
+        return output * x_mask
+
+    def infer(self, x, g=None, **kwargs):
+        from .engine import wn_infer
+
+        return wn_infer(self, x, g)
+
+
+class ResBlock2(nn.Module):
+    """Speaker-conditioned gated residual block (modules.py:223-260)."""
+
+    def __init__(self, channels, kernel_size=3, dilation=(1, 3, 5), gin_channels=0):
+        super().__init__()
+        inter = (channels // 16) * 16
+        self.kernel_size = kernel_size
+        self.dilation = tuple(dilation)
+        self.convs1 = nn.ModuleList([
+            weight_norm(nn.Conv1d(channels, inter, kernel_size, 1, dilation=d,
+                                  padding=get_padding(kernel_size, d))) for d in dilation])
+        self.convs2 = nn.ModuleList([
+            weight_norm(nn.Conv1d(inter // 2, channels, kernel_size, 1, dilation=1,
+                                  padding=get_padding(kernel_size, 1))) for _ in dilation])
+        self.conds = nn.ModuleList([
+            weight_norm(nn.Linear(gin_channels, inter)) for _ in dilation])
+        self.apply(init_weights)
+
+    def forward(self, x, g=None):
+        if not (torch.is_grad_enabled() and (x.requires_grad or any(
+                p.requires_grad for p in self.parameters()))):
+            from .engine import resblock_infer
+
+            return resblock_infer(self, x, g)
+        for c1, c2, cs in zip(self.convs1, self.convs2, self.conds):
+            xt = c1(F.leaky_relu(x, LRELU_SLOPE))
+            xa, xb = torch.chunk(xt, 2, dim=1)
+            sa, sb = torch.chunk(cs(g), 2, dim=1)
+            xt = torch.tanh(xa + sa.unsqueeze(-1)) * torch.sigmoid(xb + sb.unsqueeze(-1))
+            x = c2(xt) + x
+        return x
+
+    def infer(self, x, g=None):
+        return self.forward(x, g)
+
+
+class Flip(nn.Module):
+    """Channel reversal between couplings (modules.py:278-289)."""
+
+    def forward(self, x, *args, reverse=False, **kwargs):
+        x = torch.flip(x, [1])
+        if not reverse:
+            return x, torch.zeros(x.size(0), dtype=x.dtype, device=x.device)
+        return x
+
+    def infer(self, x, *args, reverse=True, **kwargs):
+        return torch.flip(x, [1])
+
+
+class ResidualCouplingLayer(nn.Module):
+    """Mean-only affine coupling (modules.py:314-375)."""
+
+    def __init__(self, channels, hidden_channels, kernel_size, dilation_rate, n_layers,
+                 p_dropout=0, gin_channels=0, mean_only=False):
+        assert channels % 2 == 0, "channels should be divisible by 2"
+        super().__init__()
+        self.channels = channels
+        self.hidden_channels = hidden_channels
+        self.kernel_size = kernel_size
+        self.dilation_rate = dilation_rate
+        self.n_layers = n_layers
+        self.half_channels = channels // 2
+        self.mean_only = mean_only
+        self.pre = nn.Conv1d(self.half_channels, hidden_channels, 1)
+        self.enc = WN(hidden_channels, kernel_size, dilation_rate, n_layers, p_dropout=p_dropout,
+                      gin_channels=gin_channels)
+        self.post = nn.Conv1d(hidden_channels, self.half_channels * (2 - mean_only), 1)
+        self.post.weight.data.zero_()
+        self.post.bias.data.zero_()
+
+    def _stats(self, x0, x_mask, g):
+        h = self.pre(x0) * x_mask
+        h = self.enc(h, x_mask, g=g)
+        stats = self.post(h) * x_mask
+        if not self.mean_only:
+            m, logs = torch.split(stats, [self.half_channels] * 2, 1)
+        else:
+            m, logs = stats, torch.zeros_like(stats)
+        return m, logs
+
+    def forward(self, x, x_mask, g=None, reverse=False):
+        x0, x1 = torch.split(x, [self.half_channels] * 2, 1)
+        m, logs = self._stats(x0, x_mask, g)
+        if not reverse:
+            x1 = m + x1 * torch.exp(logs) * x_mask
+            return torch.cat([x0, x1], 1), torch.sum(logs, [1, 2])
+        x1 = (x1 - m) * torch.exp(-logs) * x_mask
+        return torch.cat([x0, x1], 1)
+
+    def infer(self, x, g, reverse=True):
+        from .engine import coupling_infer
+
+        return coupling_infer(self, x, g)
+
+
+class TorchSTFT(nn.Module):
+    """STFT front of the MR-STFT loss (modules.py:378-400).  ``stft`` returns
+    (re, im) like the reference; the loss itself goes through the fused HIP
+    magnitude kernel (vits_amd.stft_loss)."""
+
+    def __init__(self, fft_size, hop_size, win_size=None):
+        super().__init__()
+        self.fft_size = fft_size
+        self.hop_size = hop_size
+        self.win_size = win_size if win_size is not None else fft_size
+        self.register_buffer("window", torch.hann_window(self.win_size), persistent=False)
+
+    def stft(self, x):
+        spec = torch.stft(x, n_fft=self.fft_size, hop_length=self.hop_size,
+                          win_length=self.win_size, window=self.window, center=True,
+                          pad_mode="reflect", return_complex=True)
+        return spec.real, spec.imag
+
+    def istft(self, real, imag):
+        return torch.istft(torch.complex(real, imag), n_fft=self.fft_size,
+                           hop_length=self.hop_size, win_length=self.win_size,
+                           window=self.window, center=True, return_complex=False)
+
+    def mag(self, x, eps=1e-7):
+        from .ops import stft_mag
+
+        return stft_mag(x, self.window, self.fft_size, self.hop_size, self.win_size, eps=eps)

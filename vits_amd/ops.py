@@ -183,11 +183,12 @@ def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Option
               in_slope: float = 1.0, cond: Optional[torch.Tensor] = None, cond_offset: int = 0,
               lengths: Optional[torch.Tensor] = None, t_out: int = 0,
               x_channel_offset: int = 0) -> ConvDesc:
-    assert x.dtype == torch.float32 and x.stride(2) == 1
+    assert x.dtype == torch.float32
     d = ConvDesc()
     d.x = x.data_ptr() + 4 * x_channel_offset * x.stride(1)
     d.x_bstride = x.stride(0)
     d.x_cstride = x.stride(1)
+    d.x_tstride = x.stride(2)
     d.cin = layer.cin
     d.tin = x.shape[2] if tin is None else tin
     d.in_slope = in_slope
@@ -226,13 +227,62 @@ def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Option
     return d
 
 
+def conv_flops(desc: ConvDesc, batch: int) -> int:
+    """Algorithmic FLOPs of one conv launch (2 * MACs of the convolution it
+    implements; for the polyphase conv-transpose: Cout * Tout * Cin * K/u)."""
+    cols = desc.tin if desc.epi == EPI_UPSAMPLE else desc.n_out
+    return 2 * batch * desc.m * cols * desc.cin * desc.k
+
+
+class ConvTimer:
+    """Optional per-launch timing of the conv kernel with HIP events on the
+    launch stream (used by bench.py for the roofline of the dominant kernel).
+    While active, batched launches are issued one descriptor at a time."""
+
+    active = None
+
+    def __init__(self):
+        self.records = []  # (start_event, end_event, flops)
+
+    def __enter__(self):
+        ConvTimer.active = self
+        return self
+
+    def __exit__(self, *exc):
+        ConvTimer.active = None
+        return False
+
+    def launch(self, lib, desc, batch, device):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        stream = torch.cuda.current_stream(device)
+        s.record(stream)
+        check(lib.vits_conv1d_forward(C.byref(desc), batch, stream.cuda_stream),
+              "vits_conv1d_forward")
+        e.record(stream)
+        self.records.append((s, e, conv_flops(desc, batch)))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        return dict(launches=len(ms), total_ms=float(sum(ms)), total_flops=int(sum(fl)),
+                    avg_ms=float(sum(ms) / max(1, len(ms))))
+
+
 def conv1d_launch(desc: ConvDesc, batch: int, device: torch.device):
     lib = _lib.load()
+    if ConvTimer.active is not None:
+        return ConvTimer.active.launch(lib, desc, batch, device)
     check(lib.vits_conv1d_forward(C.byref(desc), batch, _stream_ptr(device)), "vits_conv1d_forward")
 
 
 def conv1d_launch_seq(descs, batch: int, device: torch.device):
     lib = _lib.load()
+    if ConvTimer.active is not None:
+        for d in descs:
+            ConvTimer.active.launch(lib, d, batch, device)
+        return
     arr = (ConvDesc * len(descs))(*descs)
     check(lib.vits_conv1d_forward_seq(arr, len(descs), batch, _stream_ptr(device)),
           "vits_conv1d_forward_seq")
@@ -245,7 +295,6 @@ def conv1d(x: torch.Tensor, layer: PackedConv, *, in_slope: float = 1.0, act: in
            post_div: float = 1.0, t_out: Optional[int] = None) -> torch.Tensor:
     """Run one packed conv on [B, cin, T] fp32 (device) and return [B, out_channels, T_out]."""
     require_device(x, cond, residual, lengths)
-    x = x.contiguous() if x.stride(2) != 1 else x
     B, _, T = x.shape
     if layer.epi == EPI_UPSAMPLE:
         T_out = T * layer.up_u if t_out is None else t_out
@@ -284,7 +333,8 @@ def linear_rows(g: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
 
 
 def expand_prior(attn: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor, noise: torch.Tensor,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, exp_s: bool = False,
+                 noise_scale: float = 1.0) -> torch.Tensor:
     require_device(attn, m_p, s_p, noise)
     attn = attn.contiguous().float()
     m_p = m_p.contiguous().float()
@@ -296,7 +346,8 @@ def expand_prior(attn: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor, noise
         out = torch.empty(B, Cc, Ty, device=attn.device, dtype=torch.float32)
     lib = _lib.load()
     check(lib.vits_expand_prior(attn.data_ptr(), m_p.data_ptr(), s_p.data_ptr(), noise.data_ptr(),
-                                out.data_ptr(), B, Cc, Ty, Tx, _stream_ptr(attn.device)),
+                                out.data_ptr(), B, Cc, Ty, Tx, 1 if exp_s else 0, noise_scale,
+                                _stream_ptr(attn.device)),
           "vits_expand_prior")
     return out
 
@@ -318,15 +369,24 @@ def conv_post_tanh(x: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Te
 def layer_norm_channels(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor],
                         eps: float = 1e-5, residual: Optional[torch.Tensor] = None,
                         out: Optional[torch.Tensor] = None,
-                        lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
-    require_device(x, residual)
-    x = x.contiguous()
+                        lengths: Optional[torch.Tensor] = None,
+                        post_add: Optional[torch.Tensor] = None, scale: float = 1.0,
+                        pos: Optional[torch.Tensor] = None,
+                        pos_alpha: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = ((LN(x + residual) * gamma + beta) + post_add[b]) * scale + pos[t] * alpha,
+    zeroed at t >= lengths[b]; x, residual, out are [B, C, T] contiguous."""
+    require_device(x, residual, lengths, post_add, pos, pos_alpha)
+    assert x.is_contiguous() and (residual is None or residual.is_contiguous())
     B, Cc, T = x.shape
     if out is None:
         out = torch.empty_like(x)
+    if pos is not None:
+        assert pos.is_contiguous() and pos.shape[-1] == Cc and pos.numel() >= T * Cc
     lib = _lib.load()
     check(lib.vits_layer_norm_channels(x.data_ptr(), _ptr(residual), _ptr(gamma), _ptr(beta),
                                        out.data_ptr(), B, Cc, T, eps, _ptr(lengths),
+                                       _ptr(post_add), 0 if post_add is None else post_add.stride(0),
+                                       scale, _ptr(pos), _ptr(pos_alpha),
                                        _stream_ptr(x.device)), "vits_layer_norm_channels")
     return out
 
@@ -340,10 +400,10 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, n_heads: int,
     assert q.stride() == k.stride() == v.stride() and q.stride(2) == 1 and q.stride(1) == T
     if out is None:
         out = torch.empty(B, Cc, T, device=q.device, dtype=torch.float32)
-    assert out.stride() == q.stride()
+    assert out.stride(2) == 1 and out.stride(1) == T
     lib = _lib.load()
     check(lib.vits_attention_forward(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B,
-                                     n_heads, D, T, q.stride(0), _ptr(lengths),
+                                     n_heads, D, T, q.stride(0), out.stride(0), _ptr(lengths),
                                      _stream_ptr(q.device)), "vits_attention_forward")
     return out
 
