@@ -25,6 +25,9 @@
 
 namespace {
 
+// internal epilogue variant: STORE with a second output descriptor (row split)
+constexpr int EPI_STORE2 = 100;
+
 struct OutDesc {
   float* y;
   int64_t y_bstride;
@@ -56,8 +59,28 @@ __device__ __forceinline__ void store_std(const OutDesc& o, int b, int ch, int t
   *dst = v;
 }
 
+// Register budget of the global->LDS prefetch (per thread): the host packs
+// layers so that kc*k*BM <= VITS_W_TILE and kc*xw_pad <= VITS_X_TILE floats.
+// W chunks go global->LDS by LDS-DMA (no registers); X chunks are staged
+// through registers (zero padding + leaky-relu prologue on the way).
+constexpr int VITS_W_TILE = 4096;
+template <int BN>
+struct XTile {
+  static constexpr int floats = BN <= 128 ? 2048 : 4096;
+  static constexpr int regs = floats / 256;
+};
+typedef __attribute__((address_space(3))) void* lds_void_t;
+
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float fast_tanh(float x) {
+  // tanh(x) = 2 sigmoid(2x) - 1 ; |err| ~ 1e-7 absolute
+  return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
+}
+
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI>
-__global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc p) {
+__global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_desc p) {
   constexpr int WM = BM / WAVES_M;
   constexpr int WN = BN / WAVES_N;
   constexpr int TM = WM / 32;
@@ -69,11 +92,14 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc
   const int kc = p.kc;
   const int k = p.k;
   const int dil = p.dil;
-  const int halo = (k - 1) * dil;
-  const int xw = BN + halo;
+  const int xw = BN + (k - 1) * dil;
   const int xw_pad = (xw + 3) & ~3;
-  float* ws = smem;                  // [kc*k][BM]
-  float* xs = smem + kc * k * BM;    // [kc][xw_pad]
+  const int wrows = kc * k;
+  const int wsz = wrows * BM;
+  const int xsz = kc * xw_pad;
+  // two stages: [W0][X0][W1][X1]
+  float* const stage0 = smem;
+  float* const stage1 = smem + wsz + xsz;
 
   const int b = blockIdx.z;
   const int n0 = blockIdx.x * BN;
@@ -99,52 +125,135 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc
   const int xstart = n0 - p.pad_left;
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
-  const int wrows = kc * k;
-  constexpr int BM4 = BM / 4;
+  const float inv_xw = 1.0f / (float)xw_pad;
 
-  for (int c0 = 0; c0 < p.cin_pad; c0 += kc) {
-    // ---- stage packed weights W[c0 .. c0+kc)[0..k)[m0 .. m0+BM) ----------
+  constexpr int MAXX = XTile<BN>::regs;
+  float xreg[MAXX];
+
+  // ---- W chunk: LDS-DMA, one 1 KiB piece (256 floats) per wave instruction;
+  // lane l of piece q lands at LDS float q*256 + 4l (lane-linear image)
+  auto wdma = [&](int c0, float* st) {
     const float* wsrc = p.w + (int64_t)c0 * k * p.m_pad + m0;
-    for (int i = tid; i < wrows * BM4; i += 256) {
-      const int r = i / BM4;
-      const int q = i - r * BM4;
-      const float4 v = *reinterpret_cast<const float4*>(wsrc + (int64_t)r * p.m_pad + q * 4);
-      *reinterpret_cast<float4*>(ws + r * BM + q * 4) = v;
+    const int pieces = (wsz + 255) >> 8;
+    for (int q = wid; q < pieces; q += 4) {
+      const int e = q * 256 + lane * 4;
+      if (e < wsz) {
+        const int r = e / BM;
+        const int col = e - r * BM;
+        __builtin_amdgcn_global_load_lds(wsrc + (int64_t)r * p.m_pad + col,
+                                         (lds_void_t)(st + q * 256), 16, 0, 0);
+      }
     }
-    // ---- stage input window with zero padding + leaky-relu prologue ------
-    for (int c = 0; c < kc; ++c) {
-      const int cc = c0 + c;
-      const float* xr = xb + (int64_t)cc * p.x_cstride;
-      const bool crow = cc < p.cin;
-      for (int t = tid; t < xw_pad; t += 256) {
+  };
+  // ---- X chunk: global -> registers -------------------------------------------
+  auto gload = [&](int c0) {
+#pragma unroll
+    for (int q = 0; q < MAXX; ++q) {
+      const int i = tid + q * 256;
+      float v = 0.f;
+      if (i < xsz) {
+        const int c = __float2int_rd(((float)i + 0.5f) * inv_xw);
+        const int t = i - c * xw_pad;
+        const int cc = c0 + c;
         const int tt = xstart + t;
-        float v = 0.f;
-        if (crow && t < xw && tt >= 0 && tt < p.tin) {
-          v = xr[tt * xts];
+        if (cc < p.cin && t < xw && tt >= 0 && tt < p.tin) {
+          v = xb[(int64_t)cc * p.x_cstride + tt * xts];
           if (act_in) v = v < 0.f ? v * slope : v;
         }
-        xs[c * xw_pad + t] = v;
       }
+      xreg[q] = v;
     }
-    __syncthreads();
+  };
+  // ---- registers -> LDS stage ------------------------------------------------
+  auto lstore = [&](float* st) {
+    float* xs = st + wsz;
+#pragma unroll
+    for (int q = 0; q < MAXX; ++q) {
+      const int i = tid + q * 256;
+      if (i < xsz) xs[i] = xreg[q];
+    }
+  };
 
-    // ---- MFMA over (tap, channel pair) -------------------------------------
-    for (int j = 0; j < k; ++j) {
-      const int xoff = wn + l32 + j * dil;
-      for (int c = 0; c < kc; c += 2) {
-        const int cr = c + lhi;
-        float a[TM], bv[TN];
-#pragma unroll
-        for (int mi = 0; mi < TM; ++mi) a[mi] = ws[(cr * k + j) * BM + wm + mi * 32 + l32];
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni) bv[ni] = xs[cr * xw_pad + xoff + ni * 32];
-#pragma unroll
-        for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < TN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mi], bv[ni], acc[mi][ni], 0, 0, 0);
-      }
+  const int nchunks = p.cin_pad / kc;
+  const int half = kc >> 1;
+  const int steps = k * half;  // MFMA k-steps per chunk
+
+  wdma(0, stage0);
+  gload(0);
+  lstore(stage0);
+  __syncthreads();
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    float* cur = (ch & 1) ? stage1 : stage0;
+    float* nxt = (ch & 1) ? stage0 : stage1;
+    const bool more = ch + 1 < nchunks;
+    if (more) {  // both in flight under the MFMAs below
+      wdma((ch + 1) * kc, nxt);
+      gload((ch + 1) * kc);
     }
+
+    const float* ws = cur;
+    const float* xs = cur + wsz;
+    // k-step s = (tap j, channel pair cp), cp fastest: A rows (2cp + lhi)*k + j
+    // of W, B row 2cp + lhi of X shifted by j*dil.  Two register sets ping-
+    // pong so the LDS reads of step s+1 are in flight under the MFMAs of s;
+    // the read after the last step runs past the chunk into padded LDS and
+    // is never consumed.
+    const float* wa = ws + lhi * k * BM + wm + l32;
+    const float* xa = xs + lhi * xw_pad + wn + l32;
+    const int sa = 2 * k * BM;
+    const int sb = 2 * xw_pad;
+    int j = 0, cp = 0;
+    const float* pa = wa;
+    const float* pb = xa;
+    auto advance = [&]() {
+      ++cp;
+      pa += sa;
+      pb += sb;
+      if (cp == half) {
+        cp = 0;
+        ++j;
+        pa = wa + j * BM;
+        pb = xa + j * dil;
+      }
+    };
+    float a0[TM], b0[TN], a1[TM], b1[TN];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
+    advance();
+    int s = 0;
+    for (; s + 2 <= steps; s += 2) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) a1[mi] = pa[mi * 32];
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) b1[ni] = pb[ni * 32];
+      advance();
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
+      advance();
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[mi], b1[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (s < steps) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (more) lstore(nxt);
     __syncthreads();
   }
 
@@ -181,7 +290,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc
                 va += cond[q];
                 vb += cond[H + q];
               }
-              float v = tanhf(va) * (1.0f / (1.0f + expf(-vb)));
+              float v = fast_tanh(va) * fast_sigmoid(vb);
               store_std(o0, b, q, n, v, n >= len_b);
             }
           }
@@ -202,7 +311,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc
             }
           }
         }
-      } else {
+      } else if (EPI == EPI_STORE2) {
         OutDesc o1{p.out1.y, p.out1.y_bstride, p.out1.y_cstride, p.out1.act, p.out1.res,
                    p.out1.res_bstride, p.out1.res_cstride, p.out1.res_scale,
                    p.out1.accumulate, p.out1.post_div};
@@ -221,6 +330,54 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(const vits_conv1d_desc
             }
           }
         }
+      } else {
+        // single-output STORE: every residual / accumulator load of this
+        // 32x32 sub-tile is issued before the first store, so the 16 round
+        // trips overlap (res may alias y: each element is still read before
+        // it is written, by the same lane).
+        if (n < p.n_out) {
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + (r & 3) + 8 * (r >> 2);
+            const bool ok = row < p.m;
+            float t = acc[mi][ni][r];
+            if (p.bias) t += ok ? p.bias[row] : 0.f;
+            if (cond) t += ok ? cond[row] : 0.f;
+            v[r] = apply_act(t, o0.act);
+          }
+          float* yb = o0.y + (int64_t)b * o0.y_bstride + n;
+          if (o0.res) {
+            const float* rb = o0.res + (int64_t)b * o0.res_bstride + n;
+            float rv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + (r & 3) + 8 * (r >> 2);
+              rv[r] = row < p.m ? rb[(int64_t)row * o0.res_cstride] : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = rv[r] + o0.res_scale * v[r];
+          }
+          if (o0.accumulate) {
+            float yo[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + (r & 3) + 8 * (r >> 2);
+              yo[r] = row < p.m ? yb[(int64_t)row * o0.y_cstride] : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = yo[r] + v[r];
+          }
+          const bool msk = n >= len_b;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + (r & 3) + 8 * (r >> 2);
+            float t = v[r];
+            if (o0.post_div != 1.0f) t = t / o0.post_div;
+            if (msk) t = 0.f;
+            if (row < p.m) yb[(int64_t)row * o0.y_cstride] = t;
+          }
+        }
       }
     }
   }
@@ -230,13 +387,19 @@ template <int BM, int BN, int WM_, int WN_>
 int launch_tile(const vits_conv1d_desc& d, int batch, hipStream_t s) {
   const int halo = (d.k - 1) * d.dil;
   const int xw_pad = (BN + halo + 3) & ~3;
-  const size_t lds = sizeof(float) * ((size_t)d.kc * d.k * BM + (size_t)d.kc * xw_pad);
-  if (lds > 160 * 1024) return VITS_E_UNSUP;
+  const size_t wsz = (size_t)d.kc * d.k * BM;
+  const size_t xsz = (size_t)d.kc * xw_pad;
+  if (wsz > (size_t)VITS_W_TILE || xsz > (size_t)XTile<BN>::floats) return VITS_E_UNSUP;
+  // + tail pad: the software pipeline reads one k-step past the last chunk
+  const size_t lds = sizeof(float) * (2 * (wsz + xsz) + 2 * (size_t)d.k * BM + 2 * xw_pad + 64);
   dim3 grid((d.n_out + BN - 1) / BN, (d.m + BM - 1) / BM, batch);
   dim3 block(256);
   switch (d.epi) {
     case VITS_EPI_STORE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE>), grid, block, lds, s, d);
+      if (d.split < d.m)
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2>), grid, block, lds, s, d);
+      else
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE>), grid, block, lds, s, d);
       break;
     case VITS_EPI_GATE:
       hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE>), grid, block, lds, s, d);

@@ -62,10 +62,23 @@ def _pick_tile(m: int) -> int:
     return TILE_32x256
 
 
-def _pick_kc(cin: int, k: int, bm: int) -> int:
-    budget = max(2, (8192 // bm) // k)  # kc * k * BM * 4 bytes <= 32 KiB
-    kc = min(32, budget, cin + (cin & 1))
-    kc = max(2, kc - (kc & 1))
+TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256}
+W_TILE_FLOATS = 4096                                   # conv1d.hip VITS_W_TILE
+X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>
+
+
+def _pick_kc(cin: int, k: int, dil: int, tile: int) -> int:
+    """Input channels per K-chunk: the largest even kc within the kernel's
+    per-stage LDS/register budgets (W chunk kc*k*BM floats, X chunk
+    kc*xw_pad floats)."""
+    bm, bn = TILE_ROWS[tile], TILE_COLS[tile]
+    xw_pad = (bn + (k - 1) * dil + 3) // 4 * 4
+    budget = min(32, W_TILE_FLOATS // (k * bm), X_TILE_FLOATS[bn] // xw_pad, cin + (cin & 1))
+    budget = max(2, budget - (budget & 1))
+    # zero-padded channels cost MFMA work, each chunk costs a fixed overhead
+    # (~2 channels' worth): minimise ceil(cin/kc) * (kc + 2)
+    kc = min(range(2, budget + 1, 2), key=lambda c: (-(-cin // c) * (c + 2), -(-cin // c) * c, -c))
+    assert kc * k * bm <= W_TILE_FLOATS and kc * xw_pad <= X_TILE_FLOATS[bn], (cin, k, dil, tile)
     return kc
 
 
@@ -97,10 +110,10 @@ class PackedConv:
         return self.w.shape[0]
 
 
-def _finish_pack(rows_w: torch.Tensor, k: int, tile: int) -> tuple[torch.Tensor, int]:
+def _finish_pack(rows_w: torch.Tensor, k: int, tile: int, dil: int = 1) -> tuple[torch.Tensor, int]:
     """rows_w: [m, cin, k] -> packed [cin_pad, k, m_pad]."""
     m, cin, _ = rows_w.shape
-    kc = _pick_kc(cin, k, TILE_ROWS[tile])
+    kc = _pick_kc(cin, k, dil, tile)
     cin_pad = (cin + kc - 1) // kc * kc
     m_pad = (m + 127) // 128 * 128
     packed = rows_w.new_zeros(cin_pad, k, m_pad, dtype=torch.float32)
@@ -124,7 +137,7 @@ def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], *, dilation: i
     else:
         rows, epi, outc = w, EPI_STORE, cout
     tile = _pick_tile(cout)
-    packed, kc = _finish_pack(rows, k, tile)
+    packed, kc = _finish_pack(rows, k, tile, dilation)
     b = None if bias is None else bias.detach().to(torch.float32).contiguous()
     return PackedConv(packed, b, cin, cout, k, dilation, padding, epi, tile, kc,
                       out_channels=outc)
