@@ -97,6 +97,21 @@ def cpu_baseline(model, Tx, Ty, budget_s=12.0):
                       f"oracle/vits_oracle.py torch-CPU fp32, torch.set_num_threads({cores})"}
 
 
+def pmc_traffic():
+    """HBM bytes per conv launch from the newest committed PMC summary
+    (profiles/<tag>_summary.json, written by tools/summarize_profiles.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes); None if absent."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    c = d.get("conv1d_mfma_kernel", {})
+    return c.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,10 +173,12 @@ def main():
             s = timer.summary()
             per_launch_flops = s["total_flops"] / max(1, s["launches"])
             achieved = (s["total_flops"] / 1e12) / (s["total_ms"] / 1e3)
+            traffic, tsrc = pmc_traffic()
             roof = {"bound": "mfma", "kernel": "conv1d_mfma_kernel (all conv launches of a step)",
                     "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                    "traffic": None, "launches_per_step": s["launches"] // args.steps,
+                    "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
+                    "traffic_source": tsrc, "launches_per_step": s["launches"] // args.steps,
                     "avg_launch_ms": round(s["avg_ms"], 4),
                     "flops_per_launch": int(per_launch_flops),
                     "conv_ms_per_step": round(s["total_ms"] / args.steps, 3)}
