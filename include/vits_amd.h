@@ -66,6 +66,7 @@ extern "C" {
 #define VITS_TILE_128x128 0
 #define VITS_TILE_64x256 1
 #define VITS_TILE_32x256 2
+#define VITS_TILE_64x128 3  /* chosen by the library for small grids of 128x128 layers */
 
 typedef struct vits_conv_out {
   float* y;               /* output [B][*][y_cstride]                        */

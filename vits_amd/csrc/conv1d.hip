@@ -64,6 +64,10 @@ __device__ __forceinline__ void store_std(const OutDesc& o, int b, int ch, int t
 // W chunks go global->LDS by LDS-DMA (no registers); X chunks are staged
 // through registers (zero padding + leaky-relu prologue on the way).
 constexpr int VITS_W_TILE = 4096;
+// X staging: element i of the chunk's [kc][xw_pad] window (LDS float i) is
+// owned by thread i % 256; its (row, column) -> global offset mapping does
+// not depend on the chunk, so it is computed once per workgroup.  The host
+// keeps kc * xw_pad <= floats.
 template <int BN>
 struct XTile {
   static constexpr int floats = BN <= 128 ? 2048 : 4096;
@@ -125,10 +129,20 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   const int xstart = n0 - p.pad_left;
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
-  const float inv_xw = 1.0f / (float)xw_pad;
-
   constexpr int MAXX = XTile<BN>::regs;
   float xreg[MAXX];
+  int xrow[MAXX];  // window row of element tid + 256q (1<<24 when it is padding)
+  int xoff[MAXX];  // its global offset relative to row 0 of the chunk
+#pragma unroll
+  for (int q = 0; q < MAXX; ++q) {
+    const int i = tid + q * 256;
+    const int r = i / xw_pad;
+    const int t = i - r * xw_pad;
+    const int tt = xstart + t;
+    const bool ok = i < xsz && t < xw && tt >= 0 && tt < p.tin;
+    xrow[q] = ok ? r : (1 << 24);
+    xoff[q] = ok ? r * p.x_cstride + tt * (int)xts : 0;
+  }
 
   // ---- W chunk: LDS-DMA, one 1 KiB piece (256 floats) per wave instruction;
   // lane l of piece q lands at LDS float q*256 + 4l (lane-linear image)
@@ -145,21 +159,16 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
       }
     }
   };
-  // ---- X chunk: global -> registers -------------------------------------------
+  // ---- X chunk: global -> registers (zero padding + leaky-relu prologue) ------
   auto gload = [&](int c0) {
+    const float* base = xb + (int64_t)c0 * p.x_cstride;
+    const int lim = p.cin - c0;  // rows >= lim are channel padding
 #pragma unroll
     for (int q = 0; q < MAXX; ++q) {
-      const int i = tid + q * 256;
       float v = 0.f;
-      if (i < xsz) {
-        const int c = __float2int_rd(((float)i + 0.5f) * inv_xw);
-        const int t = i - c * xw_pad;
-        const int cc = c0 + c;
-        const int tt = xstart + t;
-        if (cc < p.cin && t < xw && tt >= 0 && tt < p.tin) {
-          v = xb[(int64_t)cc * p.x_cstride + tt * xts];
-          if (act_in) v = v < 0.f ? v * slope : v;
-        }
+      if (xrow[q] < lim) {
+        v = base[xoff[q]];
+        if (act_in) v = v < 0.f ? v * slope : v;
       }
       xreg[q] = v;
     }
@@ -390,6 +399,9 @@ int launch_tile(const vits_conv1d_desc& d, int batch, hipStream_t s) {
   const size_t wsz = (size_t)d.kc * d.k * BM;
   const size_t xsz = (size_t)d.kc * xw_pad;
   if (wsz > (size_t)VITS_W_TILE || xsz > (size_t)XTile<BN>::floats) return VITS_E_UNSUP;
+  // 32-bit window offsets
+  if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
+    return VITS_E_UNSUP;
   // + tail pad: the software pipeline reads one k-step past the last chunk
   const size_t lds = sizeof(float) * (2 * (wsz + xsz) + 2 * (size_t)d.k * BM + 2 * xw_pad + 64);
   dim3 grid((d.n_out + BN - 1) / BN, (d.m + BM - 1) / BM, batch);
@@ -431,8 +443,16 @@ int conv1d_one(const vits_conv1d_desc& d, int batch, hipStream_t s) {
   int rc = check_desc(d, batch);
   if (rc) return rc;
   switch (d.tile) {
-    case VITS_TILE_128x128:
+    case VITS_TILE_128x128: {
+      // a 128x128 grid that cannot fill the chip twice over (256 CUs) runs
+      // as 64x128 tiles: same packing (its W/X budgets are a subset), twice
+      // the workgroups
+      const long blocks = (long)((d.n_out + 127) / 128) * ((d.m + 127) / 128) * batch;
+      if (blocks < 512) return launch_tile<64, 128, 2, 2>(d, batch, s);
       return launch_tile<128, 128, 2, 2>(d, batch, s);
+    }
+    case VITS_TILE_64x128:
+      return launch_tile<64, 128, 2, 2>(d, batch, s);
     case VITS_TILE_64x256:
       return launch_tile<64, 256, 1, 4>(d, batch, s);
     case VITS_TILE_32x256:

@@ -62,9 +62,9 @@ def _pick_tile(m: int) -> int:
     return TILE_32x256
 
 
-TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256}
+TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, 3: 128}
 W_TILE_FLOATS = 4096                                   # conv1d.hip VITS_W_TILE
-X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>
+X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::floats
 
 
 def _pick_kc(cin: int, k: int, dil: int, tile: int) -> int:
