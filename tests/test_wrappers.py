@@ -1,0 +1,82 @@
+"""Inference wrappers: export.load_model (greedy soup), EmoVITS, VITSWrap."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from common import build_model, tiny_cfg
+
+
+def _write_ckpts(tmp_path, n=3):
+    c = tiny_cfg()
+    hps = {"train": {"segment_size": c["data"]["segment_size"] * 192},
+           "data": {"text_channels": c["data"]["text_channels"],
+                    "filter_length": (c["data"]["spec_channels"] - 1) * 2, "hop_length": 192,
+                    "n_speakers": c["data"]["n_speakers"], "sampling_rate": 16000,
+                    "noise_scale": 0.707},
+           "model": c["model"]}
+    with open(tmp_path / "config.json", "w") as f:
+        json.dump(hps, f)
+    sds = []
+    for i in range(n):
+        m = build_model(c["model"], c["data"], fill=False)
+        from vits_amd.utils import deterministic_fill_
+
+        deterministic_fill_(m, seed=100 + i)
+        torch.save({"model": m.state_dict(), "iteration": i}, tmp_path / f"G_{(i + 1) * 1000}.pth")
+        sds.append(m.state_dict())
+    return hps, sds
+
+
+def test_load_model_greedy_soup(tmp_path):
+    from vits_amd.export import load_model
+
+    _, sds = _write_ckpts(tmp_path, 3)
+    m = load_model(str(tmp_path), greedy=5)
+    sd = m.state_dict()
+    k = "dec.conv_pre.weight"
+    want = (sds[0][k] + sds[1][k] + sds[2][k]) / 3
+    # reference order: last file first, then the others in sorted order
+    assert torch.allclose(sd[k], want, atol=1e-6)
+    m1 = load_model(str(tmp_path / "G_3000.pth"))
+    assert torch.equal(m1.state_dict()[k], sds[2][k])
+
+
+def test_wav_header():
+    from vits_amd.vits_wrap import _gen_wav_header
+
+    h = _gen_wav_header(100, 16000, 16)
+    assert len(h) == 44 and h[:4] == b"RIFF" and h[8:12] == b"WAVE" and h[36:40] == b"data"
+
+
+@pytest.mark.gpu
+def test_emovits_and_vitswrap(tmp_path, device):
+    from vits_amd.infer import EmoVITS
+    from vits_amd.vits_wrap import VITSWrap
+
+    _write_ckpts(tmp_path, 1)
+    c = tiny_cfg()
+    np.random.seed(0)
+    emo_bank = np.random.randn(3, 1024).astype(np.float32)
+    emo_bank.tofile(tmp_path / "1.emo")
+    with open(tmp_path / "spk.map", "w") as f:
+        f.write("7 1\n")
+    tts = EmoVITS(str(tmp_path / "G_1000.pth"), device)
+    assert tts.spkid_mapping == {7: 1}
+    text = np.random.randn(9, c["data"]["text_channels"]).astype(np.float32)
+    wav, emo = tts.infer(7, text, None)
+    assert wav.dtype == np.float32 and wav.ndim == 1 and len(wav) % 192 == 0 and len(wav) > 0
+    assert np.isfinite(wav).all() and np.abs(wav).max() <= 1.0
+
+    class Parser:
+        max_utt_length = 10
+
+        def __call__(self, utt_id, text):
+            return utt_id, text, np.random.randn(max(1, len(text)), c["data"]["text_channels"]).astype(np.float32)
+
+    wrap = VITSWrap(textparser=Parser(), speecher=tts)
+    out = wrap.speaking({"text": "abcdefghij。klmnopq", "spkid": 1, "sampling_rate": 22050, "pitch": 1.2})
+    assert out["sr"] == 22050 and out["wav"][:4] == b"RIFF"
+    assert len(out["segment_info"]) == 2 and out["rtf"] > 0

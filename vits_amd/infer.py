@@ -1,0 +1,178 @@
+"""EmoVITS inference wrapper (reference ``infer.py``), on the HIP engine.
+
+Same constructor and ``infer`` contract as ``infer.py:12-184``: speaker-id
+mapping files ``*.map``, per-speaker emotion banks ``{spk}.emo`` next to the
+checkpoint, an fp16 model (``.half()`` like the reference; the HIP plans
+compute in fp32 internally and hand back the model dtype), a fixed noise
+buffer sliced at a random offset per call.  Differences: the noise buffer
+lives on the device (no host->device copy per call) and the CLI writes WAVs
+with scipy instead of soundfile.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+from . import utils
+from .commons import infer_path
+from .export import load_model
+
+
+class EmoVITS(object):
+    def __init__(self, checkpoint_path=None, device=None, *, loglv=0, hps=None, model=None):
+        self.loglv = loglv
+        if checkpoint_path is None and model is None:
+            checkpoint_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "checkpoint",
+                                           "checkpoint.pth")
+        self.res_root_path = os.path.dirname(checkpoint_path) if checkpoint_path else "."
+        if hps is None:
+            hps = utils.get_hparams_from_file(os.path.join(self.res_root_path, "config.json"))
+        self.hps = hps
+        self.sampling_rate = hps.data["sampling_rate"]
+        self.hop_size = hps.data["hop_length"]
+        self.text_channels = hps.data["text_channels"]
+        self.inter_channels = hps.model["inter_channels"]
+        self.num_speaker = hps.data["n_speakers"]
+        self.noise_scale = hps.data["noise_scale"]
+
+        self.spkid_mapping, self.spkid_mapping_mtime = {}, {}
+        for map_path in utils.find_files(self.res_root_path, "*.map"):
+            self._load_spkid_mapping(map_path)
+        self.spk_emo_embed, self.spk_emo_embed_mtime = {}, {}
+        for emo_path in utils.find_files(self.res_root_path, "*.emo"):
+            self._load_spk_emo_embed(int(os.path.splitext(os.path.basename(emo_path))[0]))
+
+        if isinstance(device, str):
+            device = torch.device(device)
+        self.device = device if device is not None else torch.device("cuda")
+        if model is None:
+            model = load_model(checkpoint_path, hps)
+        model.remove_weight_norm()
+        self.model = model.half().eval().to(self.device)
+        self.noise = (torch.randn(1 * self.inter_channels * 4096) * self.noise_scale).half().to(self.device)
+        self.inference = self.infer
+
+    # -- speaker / emotion banks (infer.py:77-133) ----------------------------
+    def _load_spkid_mapping(self, mapfn):
+        if not os.path.exists(mapfn):
+            return
+        with open(mapfn, "rt") as f:
+            for line in f:
+                line = line.strip()
+                if not line or line[0] == "#":
+                    continue
+                arr = line.split()
+                if len(arr) != 2 or not (arr[0].isdigit() and arr[1].isdigit()):
+                    continue
+                self.spkid_mapping[int(arr[0])] = int(arr[1])
+        self.spkid_mapping_mtime[mapfn] = int(os.stat(mapfn).st_mtime)
+
+    def _load_spk_emo_embed(self, spkid: int):
+        emo_path = os.path.join(self.res_root_path, f"{spkid}.emo")
+        if os.path.exists(emo_path):
+            emb = torch.from_numpy(np.fromfile(emo_path, dtype=np.float32).reshape(-1, 1024)).half()
+            self.spk_emo_embed[spkid] = emb
+            self.spk_emo_embed_mtime[emo_path] = int(os.stat(emo_path).st_mtime)
+            return emb
+        return None
+
+    def _get_spk_emo_embed(self, emo: tuple):
+        if isinstance(emo[0], (int, np.integer)):
+            emb = self.spk_emo_embed.get(int(emo[0]))
+            if emb is None:
+                emb = self._load_spk_emo_embed(int(emo[0]))
+            assert emb is not None, f"no emotion bank for speaker {emo[0]}"
+        elif isinstance(emo[0], np.ndarray):
+            emb = torch.from_numpy(emo[0].reshape(-1, 1024).astype(np.float32)).half()
+        else:
+            raise ValueError("emo[0] must be int or ndarray")
+        eid = -1 if len(emo) == 1 else int(emo[1])
+        if eid < 0 or eid > emb.size(0):
+            eid = np.random.randint(0, emb.size(0))
+        return emb[eid]
+
+    def update(self):
+        for map_path in list(self.spkid_mapping_mtime.keys()):
+            if not os.path.exists(map_path):
+                self.spkid_mapping_mtime.pop(map_path)
+                continue
+            if int(os.stat(map_path).st_mtime) != self.spkid_mapping_mtime[map_path]:
+                self._load_spkid_mapping(map_path)
+        for emo_path in list(self.spk_emo_embed_mtime.keys()):
+            if not os.path.exists(emo_path):
+                self.spk_emo_embed_mtime.pop(emo_path)
+                continue
+            if int(os.stat(emo_path).st_mtime) != self.spk_emo_embed_mtime[emo_path]:
+                self._load_spk_emo_embed(int(os.path.splitext(os.path.basename(emo_path))[0]))
+
+    # -- synthesis (infer.py:135-184) ------------------------------------------
+    @torch.no_grad()
+    def infer(self, spkid, text, emo, *, duration_rate=1.0):
+        x_length = text.shape[0]
+        spkid = self.spkid_mapping.get(spkid, spkid)
+        assert spkid < self.num_speaker, f"spkid={spkid} must be less than {self.num_speaker}"
+        sid = torch.tensor([spkid], dtype=torch.long, device=self.device)
+        if isinstance(emo, torch.Tensor):
+            emo = emo.half()
+        else:
+            if emo is None:
+                emo = (spkid, -1)
+            if isinstance(emo[0], (int, np.integer)):
+                emo = tuple([self.spkid_mapping.get(emo[0], emo[0]) if emo[0] != 0 else spkid,
+                             -1 if len(emo) == 1 else emo[1]])
+            emo = self._get_spk_emo_embed(emo).unsqueeze(0)
+        text_t = torch.from_numpy(np.ascontiguousarray(text)).half().to(self.device).unsqueeze(0)
+        emo = emo.to(self.device)
+
+        m_p, s_p, logw, g = self.model.infer_p1(text_t, emo, sid)
+        w = torch.exp(logw) * duration_rate
+        w_ceil = torch.ceil(w)
+        y_length = int(torch.clamp_min(torch.sum(w_ceil), 1).item())
+        nl = self.inter_channels * y_length
+        start = np.random.randint(max(1, self.noise.size(0) - nl))
+        noise = self.noise[start:start + nl].view(1, self.inter_channels, y_length)
+        attn = infer_path(w_ceil.float(), x_length, y_length).half()
+        wav = self.model.infer_p2(attn, m_p, s_p, g, noise)
+        return wav.float().view(-1).cpu().numpy(), emo
+
+
+def main(argv=None):
+    import argparse
+    import time
+
+    from scipy.io import wavfile
+
+    ap = argparse.ArgumentParser(description="Decode text vectors with vits_amd (EmoVITS).")
+    ap.add_argument("--scpfn", "--scp", required=True)
+    ap.add_argument("--spkid", "--sid", default=None, type=int)
+    ap.add_argument("--outdir", required=True)
+    ap.add_argument("--checkpoint", "--ckpt", default=None)
+    ap.add_argument("--device", default=None)
+    args = ap.parse_args(argv)
+    os.makedirs(args.outdir, exist_ok=True)
+    model = EmoVITS(args.checkpoint, args.device, loglv=1)
+    total_rtf, n = 0.0, 0
+    with open(args.scpfn) as fid:
+        for line in fid:
+            line = line.strip()
+            if not line or line[0] == "#":
+                continue
+            parts = line.split("|")
+            utt_id = os.path.splitext(os.path.basename(parts[0]))[0]
+            spkid = int(args.spkid) if args.spkid is not None else (int(parts[-1]) if len(parts) > 1 else 1)
+            start = time.time()
+            text = np.fromfile(parts[0], dtype=np.float32).reshape(-1, model.text_channels)
+            wav, _ = model.infer(spkid, text, None)
+            wavfile.write(os.path.join(args.outdir, f"{utt_id}.wav"), model.sampling_rate,
+                          np.clip(wav * 32767, -32768, 32767).astype(np.int16))
+            total_rtf += (time.time() - start) / (len(wav) / model.sampling_rate)
+            n += 1
+    sys.stderr.write(f"Finished generation of {n} utterances (RTF = {total_rtf / max(1, n):.03f}).\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

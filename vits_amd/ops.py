@@ -515,5 +515,6 @@ def stft_mag(x: torch.Tensor, window: torch.Tensor, n_fft: int, hop: int, win: i
     """sqrt(|STFT(x)|^2 + eps), [B, n_fft//2+1, frames]; differentiable in x."""
     if pad is None:
         pad = n_fft // 2
-    out = _StftMag.apply(x, window, n_fft, hop, win, pad, eps)
-    return out
+    # cast outside the Function so autograd returns the gradient in x's dtype
+    # (fp16 under autocast, as y_hat is in train_stft.py)
+    return _StftMag.apply(x.float(), window, n_fft, hop, win, pad, eps)

@@ -1,0 +1,185 @@
+"""Data-parallel training step of ``train_stft.py`` on the vits_amd modules.
+
+``TrainStep.step`` reproduces one iteration of the reference hot loop
+(train_stft.py:162-236): fp16 autocast G forward (HIP monotonic alignment
+search inside), logging mels, waveform slice, MR-STFT loss on the HIP STFT
+kernels (forward + adjoint), D forward on real / detached fake, D loss ->
+scaled backward -> unscale -> grad norm -> RAdam step; D forward on fake,
+G losses (dur, stft, kl, kl_q, adversarial) -> scaled backward -> AdamW step
+-> scaler update.  Under ``torch.distributed`` both networks are DDP-wrapped
+(train_stft.py:108-110): the only collective is DDP's bucketed gradient
+all-reduce over RCCL/xGMI (the ``nccl`` backend on ROCm).
+
+Differences from the reference, all on the host side: per-discriminator
+losses stay on the device (no ``.item()`` per loss, losses.py:28-29) and the
+grad norm is reduced on the device once (commons.py:158-173 syncs per
+parameter); RAdam is ``torch.optim.RAdam`` (same rectified-Adam update as
+radam.py).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+from torch.nn.parallel import DistributedDataParallel as DDP
+
+from . import commons, utils
+from .discriminators import MultiWaveSTFTDiscriminator
+from .losses import discriminator_loss, generator_loss, kl_loss
+from .mel_processing import mel_spectrogram_torch, spec_to_mel_torch
+from .models import SynthesizerTrn
+from .stft_loss import MultiResolutionSTFTLoss
+
+
+def build_models(hps, device):
+    net_g = SynthesizerTrn(hps.data.text_channels, hps.data.filter_length // 2 + 1,
+                           hps.train.segment_size // hps.data.hop_length,
+                           n_speakers=hps.data.n_speakers, align_noise=hps.train.align_noise,
+                           align_noise_decay=hps.train.align_noise_decay, **hps.model).to(device)
+    net_d = MultiWaveSTFTDiscriminator().to(device)
+    return net_g, net_d
+
+
+class TrainStep:
+    def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True):
+        self.hps = hps
+        self.device = device
+        self.log_mels = log_mels
+        self.mstft = MultiResolutionSTFTLoss().to(device)
+        self.optim_g = torch.optim.AdamW(net_g.parameters(), hps.train.learning_rate,
+                                         betas=hps.train.betas, weight_decay=hps.train.weight_decay,
+                                         eps=hps.train.eps)
+        self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4)
+        if ddp:
+            ids = [device.index] if device.type == "cuda" else None
+            net_g = DDP(net_g, device_ids=ids)
+            net_d = DDP(net_d, device_ids=ids)
+        self.net_g, self.net_d = net_g, net_d
+        fp16 = bool(hps.train.fp16_run) and device.type == "cuda"
+        self.autocast = lambda enabled=fp16: torch.autocast(device.type, dtype=torch.float16,
+                                                            enabled=enabled)
+        self.scaler = torch.amp.GradScaler(device.type, enabled=fp16)
+
+    def step(self, batch):
+        hps = self.hps
+        x, x_lengths, spec, spec_lengths, y, y_lengths, emo, speakers = (
+            t.to(self.device, non_blocking=True) for t in batch)
+        with self.autocast():
+            (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
+             (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
+                x, x_lengths, spec, spec_lengths, emo, speakers)
+            if self.log_mels:  # train_stft.py:173-191 (logging mels, computed every step)
+                mel = spec_to_mel_torch(spec[:1].float(), hps.data.filter_length,
+                                        hps.data.n_mel_channels, hps.data.sampling_rate,
+                                        hps.data.mel_fmin, hps.data.mel_fmax)
+                _ = commons.slice_segments(mel, ids_slice[:1], hps.train.segment_size // hps.data.hop_length)
+                with torch.no_grad():
+                    _ = mel_spectrogram_torch(y_hat[:1].squeeze(1).detach().float(), hps.data.filter_length,
+                                              hps.data.n_mel_channels, hps.data.sampling_rate,
+                                              hps.data.hop_length, hps.data.win_length,
+                                              hps.data.mel_fmin, hps.data.mel_fmax)
+            y = commons.slice_segments(y, ids_slice * hps.data.hop_length, hps.train.segment_size)
+            sc_loss, mag_loss, y_mag, y_hat_mag = self.mstft(y.squeeze(1), y_hat.squeeze(1))
+            y_d_hat_r = self.net_d(y, y_mag)
+            y_d_hat_g = self.net_d(y_hat.detach(), [m.detach() for m in y_hat_mag])
+            with self.autocast(False):
+                loss_disc, _, _ = discriminator_loss(y_d_hat_r, y_d_hat_g)
+        self.optim_d.zero_grad()
+        self.scaler.scale(loss_disc).backward()
+        self.scaler.unscale_(self.optim_d)
+        grad_norm_d = commons.clip_grad_value_(self.net_d.parameters(), None)
+        self.scaler.step(self.optim_d)
+
+        with self.autocast():
+            y_d_hat_g = self.net_d(y_hat, y_hat_mag)
+            with self.autocast(False):
+                loss_dur = torch.sum(l_length.float()) * hps.train.c_dur
+                loss_stft = (sc_loss.float() + mag_loss.float()) * hps.train.c_stft
+                loss_kl = kl_loss(z_p, logs_q, m_p, logs_p, z_mask) * hps.train.c_kl
+                loss_kl_q = kl_loss(z_q, logs_p, m_q, logs_q, z_mask) * hps.train.c_kl_q
+                loss_gen, _ = generator_loss(y_d_hat_g)
+                loss_gen_all = loss_gen + loss_stft + loss_dur + loss_kl + loss_kl_q
+        self.optim_g.zero_grad()
+        self.scaler.scale(loss_gen_all).backward()
+        self.scaler.unscale_(self.optim_g)
+        grad_norm_g = commons.clip_grad_value_(self.net_g.parameters(), None)
+        self.scaler.step(self.optim_g)
+        self.scaler.update()
+        return {"loss_disc": loss_disc.detach(), "loss_gen_all": loss_gen_all.detach(),
+                "loss_stft": loss_stft.detach(), "loss_dur": loss_dur.detach(),
+                "loss_kl": loss_kl.detach(), "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
+
+
+def default_hps():
+    """configs/base.json (the reference's shape source)."""
+    return utils.get_hparams_from_dict({
+        "train": {"log_interval": 1000, "eval_interval": 1000, "seed": 1234, "epochs": 500,
+                  "steps": 3000, "learning_rate": 2e-4, "betas": [0.8, 0.99], "eps": 1e-9,
+                  "batch_size": 32, "fp16_run": True, "lr_decay": 0.999875, "segment_size": 9216,
+                  "weight_decay": 0.01, "c_mel": 45, "c_stft": 25, "c_dur": 2, "c_kl": 1.0,
+                  "c_kl_q": 0.01, "align_noise": 1e-2, "align_noise_decay": 1e-6,
+                  "align_noise_min": 1e-4},
+        "data": {"max_text_len": 384, "max_wav_len": 192000, "text_channels": 256,
+                 "sampling_rate": 16000, "filter_length": 1024, "hop_length": 192,
+                 "win_length": 768, "n_mel_channels": 80, "mel_fmin": 0.0, "mel_fmax": None,
+                 "n_speakers": 2048, "noise_scale": 0.707},
+        "model": {"inter_channels": 192, "hidden_channels": 256, "filter_channels": 512,
+                  "n_heads": 2, "n_layers": 6, "kernel_size": 5, "p_dropout": 0.1, "ffn": "FFN2",
+                  "resblock": "2", "resblock_kernel_sizes": [3, 7, 11],
+                  "resblock_dilation_sizes": [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+                  "upsample_rates": [8, 6, 2, 2], "upsample_initial_channel": 512,
+                  "upsample_kernel_sizes": [16, 12, 4, 4], "kernel_size_q": 5, "n_layers_q": 16,
+                  "hidden_size_d": 256, "kernel_size_d": 5, "p_dropout_d": 0.5,
+                  "act_func_d": "ReLU", "act_func_params_d": {}, "use_spectral_norm": False,
+                  "dilation_rate": [1, 1, 1, 1], "n_flows": 4, "gin_channels": 1024}})
+
+
+def synthetic_batch(hps, batch, tx=100, ty=500, seed=0, ragged=False):
+    """One collated batch of SURVEY.md §8(d) C3 synthetic inputs."""
+    from .data_utils import SyntheticTextAudioSpeaker, TextAudioSpeakerCollate
+
+    ds = SyntheticTextAudioSpeaker(batch, tx=tx, ty=ty, text_channels=hps.data.text_channels,
+                                   spec_channels=hps.data.filter_length // 2 + 1,
+                                   hop=hps.data.hop_length, n_speakers=hps.data.n_speakers,
+                                   seed=seed, ty_min=300 if ragged else None)
+    return TextAudioSpeakerCollate()([ds[i] for i in range(batch)])
+
+
+def main(argv=None):
+    """Synthetic-data DDP training driver (torchrun: RANK/WORLD_SIZE/LOCAL_RANK)."""
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-c", "--config", default=None)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=None)
+    args = ap.parse_args(argv)
+    hps = utils.get_hparams_from_file(args.config) if args.config else default_hps()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank)
+    torch.manual_seed(hps.train.seed)
+    net_g, net_d = build_models(hps, device)
+    stepper = TrainStep(hps, net_g, net_d, device, ddp=world > 1)
+    bs = args.batch or hps.train.batch_size
+    batch = synthetic_batch(hps, bs, seed=rank)
+    for i in range(args.steps):
+        t0 = time.perf_counter()
+        out = stepper.step(batch)
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"step {i}: {time.perf_counter() - t0:.3f}s loss_g={float(out['loss_gen_all']):.4f} "
+                  f"loss_d={float(out['loss_disc']):.4f}", flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
