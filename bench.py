@@ -18,9 +18,16 @@ Extra fields:
                 against the fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
   cpu_baseline  the CPU oracle (oracle/vits_oracle.py, torch fp32 CPU: the
                 reference algorithm restated) on a bounded sample.
+  train         the metric's second half (BASELINE configs 3/4): train utt/s of
+                the train_stft step (vits_amd/train.py: G fwd/bwd, MWSD D,
+                HIP MAS + MR-STFT, fp16 autocast, AdamW/RAdam) at
+                --train-batch per GPU, Tx=100, Ty=500; under torchrun both
+                networks are DDP-wrapped (RCCL gradient all-reduce), weak
+                scaling, value = all ranks' utterances / slowest rank's time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
        [--tx 100] [--ty 500] [--graph] [--no-cpu-baseline]
+       [--train-batch 32] [--train-steps 5] [--train-warmup 2] [--no-train]
 """
 from __future__ import annotations
 
@@ -112,6 +119,49 @@ def pmc_traffic():
     return c.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def train_leg(args, device, rank, world, dist):
+    """Timed train_stft steps (BASELINE C3/C4) on synthetic base.json batches."""
+    from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
+
+    hps = default_hps()
+    torch.manual_seed(hps.train.seed)
+    net_g, net_d = build_models(hps, device)
+    st = TrainStep(hps, net_g, net_d, device, ddp=world > 1)
+    B = args.train_batch
+    batch = [t.to(device) for t in synthetic_batch(hps, B, tx=args.tx, ty=args.ty, seed=rank)]
+    for _ in range(args.train_warmup):
+        st.step(batch)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.train_steps):
+        out = st.step(batch)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    utt = B * world * args.train_steps
+    res = {"value": round(utt / el, 2), "unit": "utt/s", "per_gpu": round(utt / el / world, 2),
+           "ms_per_step": round(el / args.train_steps * 1e3, 2), "steps": args.train_steps,
+           "warmup": args.train_warmup, "global_batch": B * world, "dtype": "fp16 autocast",
+           "scaling": "weak",
+           "workload": f"train_stft step (G fwd/bwd + MWSD D x3 + MR-STFT + MAS) batch={B}/GPU "
+                       f"Tx={args.tx} Ty={args.ty} segment 48 frames",
+           "parallelism": f"ddp{world} (RCCL all-reduce)" if world > 1 else "single GPU",
+           "tflops_alg": round(365.4e9 * utt / el / 1e12, 2),
+           "loss_gen_all": round(float(out["loss_gen_all"]), 4),
+           "reference_cpu": "0.945 utt/s at B=4 on 8 vCPU (BASELINE.md, measured in the survey)"}
+    del st, net_g, net_d
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +173,10 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay a captured hipGraph per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--train-batch", type=int, default=32)
+    ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--train-warmup", type=int, default=2)
+    ap.add_argument("--no-train", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,6 +237,8 @@ def main():
                     "flops_per_launch": int(per_launch_flops),
                     "conv_ms_per_step": round(s["total_ms"] / args.steps, 3)}
 
+    train = None if args.no_train else train_leg(args, device, rank, world, dist)
+
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -208,6 +264,7 @@ def main():
             "rtf_16k": round((ms_per_step / 1e3) / (B * Ty * HOP / SR), 6),
             "x_realtime_22k": round(value / world / 22050.0, 1),
             "roofline": roof,
+            "train": train,
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(model, Tx, Ty)

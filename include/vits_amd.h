@@ -209,7 +209,8 @@ int vits_layer_norm_channels(const float* x, const float* r, const float* gamma,
 /* ---------------------------------------------------------------------- */
 /* scaled-dot-product attention over [B][H*D][T] channel-major q/k/v      */
 /* (batch stride qkv_bstride, e.g. slices of one fused q|k|v buffer), key */
-/* mask from lengths (fill -1e4), out [B][H*D][T] with out_bstride         */
+/* mask from lengths (fill -1e4), out [B][H*D][T] with out_bstride;        */
+/* head_dim in {16, 32, 48, 64, 96, 128}, else VITS_E_UNSUP              */
 /* ---------------------------------------------------------------------- */
 int vits_attention_forward(const float* q, const float* k, const float* v, float* out,
                            int batch, int heads, int head_dim, int t_len,

@@ -231,6 +231,22 @@ def test_attention(device, T, lens):
     _close(out, ref, tol=2e-5, what="attention")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [16, 32, 48, 64, 96])
+def test_attention_head_dims(device, D):
+    g = torch.Generator().manual_seed(D)
+    B, H, T = 2, 2, 37
+    q, k, v = (torch.randn(B, H * D, T, generator=g) for _ in range(3))
+    lengths = torch.tensor([T, 20], dtype=torch.int32)
+    mask = (torch.arange(T)[None] < lengths[:, None]).float()
+    am = (mask.unsqueeze(2) * mask.unsqueeze(1)).unsqueeze(1)
+    qh, kh, vh = (t.view(B, H, D, T).transpose(2, 3) for t in (q, k, v))
+    sc = torch.matmul(qh / D ** 0.5, kh.transpose(-2, -1)).masked_fill(am == 0, -1e4)
+    ref = torch.matmul(F.softmax(sc, -1), vh).transpose(2, 3).reshape(B, H * D, T)
+    out = ops.attention(q.to(device), k.to(device), v.to(device), H, lengths=lengths.to(device))
+    _close(out, ref, tol=2e-5, what=f"attention D={D}")
+
+
 def test_attention_fused_qkv_strides(device):
     """q|k|v as channel slices of one [B, 3C, T] projection buffer (the
     engine's layout): batch stride 3*C*T for inputs, C*T for the output."""

@@ -1,0 +1,60 @@
+"""Time the train_stft step (BASELINE C3/C4) on one GPU: base.json shapes,
+synthetic batch Tx=100 / Ty=500, fp16 autocast.  Usage:
+    python tools/train_bench.py --batch 32 --steps 5 --warmup 2
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-mels", action="store_true")
+    ap.add_argument("--torch-prof", default=None, help="write a torch.profiler op table here")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    hps = default_hps()
+    torch.manual_seed(1234)
+    g, d = build_models(hps, dev)
+    st = TrainStep(hps, g, d, dev, log_mels=not args.no_mels)
+    batch = [t.to(dev) for t in synthetic_batch(hps, args.batch, seed=0)]
+    for i in range(args.warmup):
+        t0 = time.perf_counter()
+        st.step(batch)
+        torch.cuda.synchronize()
+        print(f"warmup {i}: {time.perf_counter() - t0:.3f}s", flush=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = st.step(batch)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    if args.torch_prof:
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            st.step(batch)
+            torch.cuda.synchronize()
+        ka = prof.key_averages()
+        with open(args.torch_prof, "w") as f:
+            f.write(ka.table(sort_by="self_cuda_time_total", row_limit=60, max_name_column_width=90))
+            f.write("\n\n")
+            f.write(ka.table(sort_by="cuda_time_total", row_limit=60, max_name_column_width=90))
+    print(json.dumps({"batch": args.batch, "s_per_step": dt, "utt_per_s": args.batch / dt,
+                      "loss_g": float(out["loss_gen_all"]), "loss_d": float(out["loss_disc"]),
+                      "max_mem_gb": torch.cuda.max_memory_allocated() / 2**30}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -108,12 +108,17 @@ def clip_grad_value_(parameters, clip_value, norm_type=2):
     norm_type = float(norm_type)
     if not parameters:
         return 0.0
-    norms = torch.stack([p.grad.detach().norm(norm_type).float() for p in parameters])
+    grads = [p.grad.detach() for p in parameters]
+    if norm_type == 2.0 and grads[0].is_cuda:
+        # one multi-tensor launch per dtype/device group instead of one per parameter
+        norms = torch.stack([n.float() for n in torch._foreach_norm(grads, 2.0)])
+    else:
+        norms = torch.stack([g.norm(norm_type).float() for g in grads])
     total = torch.sum(norms ** norm_type) ** (1.0 / norm_type)
     if clip_value is not None:
         cv = float(clip_value)
-        for p in parameters:
-            p.grad.data.clamp_(min=-cv, max=cv)
+        torch._foreach_clamp_min_(grads, -cv)
+        torch._foreach_clamp_max_(grads, cv)
     return float(total.item())
 
 

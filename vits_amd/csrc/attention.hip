@@ -30,9 +30,9 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const float* __restrict__ 
                                                       float* __restrict__ out, int H, int T,
                                                       int64_t bstride, int64_t out_bstride,
                                                       const int32_t* __restrict__ lengths) {
-  static_assert(D % 32 == 0, "head dim multiple of 32");
-  constexpr int KS = D / 2;   // k-steps of the QK product
-  constexpr int DT = D / 32;  // d tiles of the PV product
+  static_assert(D % 16 == 0, "head dim multiple of 16");
+  constexpr int KS = D / 2;          // k-steps of the QK product
+  constexpr int DT = (D + 31) / 32;  // d tiles of the PV product (last one partial for D%32)
   const int lane = threadIdx.x;
   const int l32 = lane & 31;
   const int lhi = lane >> 5;
@@ -107,11 +107,12 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const float* __restrict__ 
     // O^T[d][query] += V^T[d][key] P^T[key][query]
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
+      const bool dvalid = (D % 32 == 0) || (t * 32 + l32 < D);
       const float* vr = vb + (int64_t)(t * 32 + l32) * T + k0 + 4 * lhi;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int kk = (r & 3) + 8 * (r >> 2);
-        const float a = (k0 + kk + 4 * lhi < T) ? vr[kk] : 0.f;
+        const float a = (dvalid && k0 + kk + 4 * lhi < T) ? vr[kk] : 0.f;
         o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s[r], o[t], 0, 0, 0);
       }
     }
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const float* __restrict__ 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * lhi;
-      ob[(int64_t)d * T + qi] = o[t][r] * inv;
+      if (D % 32 == 0 || d < D) ob[(int64_t)d * T + qi] = o[t][r] * inv;
     }
 }
 
@@ -141,6 +142,15 @@ extern "C" int vits_attention_forward(const float* q, const float* k, const floa
   dim3 grid((t_len + AT_Q - 1) / AT_Q, heads, batch);
   hipStream_t s = as_stream(stream);
   switch (head_dim) {
+#define VITS_ATTN_CASE(D)                                                                      \
+    case D:                                                                                    \
+      hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(64), 0, s, q, k, v, out, heads, t_len, \
+                         bstride, out_bstride, lengths);                                       \
+      break;
+    VITS_ATTN_CASE(16)
+    VITS_ATTN_CASE(32)
+    VITS_ATTN_CASE(48)
+#undef VITS_ATTN_CASE
     case 64:
       hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(64), 0, s, q, k, v, out, heads, t_len,
                          bstride, out_bstride, lengths);

@@ -52,7 +52,7 @@ class TrainStep:
         self.mstft = MultiResolutionSTFTLoss().to(device)
         self.optim_g = torch.optim.AdamW(net_g.parameters(), hps.train.learning_rate,
                                          betas=hps.train.betas, weight_decay=hps.train.weight_decay,
-                                         eps=hps.train.eps)
+                                         eps=hps.train.eps, fused=device.type == "cuda")
         self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4)
         if ddp:
             ids = [device.index] if device.type == "cuda" else None
