@@ -13,6 +13,8 @@
  *   vits_maximum_path        monotonic_align.maximum_path, call site
  *                            models.py:498 (external Cython package
  *                            `monotonic-align`, not vendored)
+ *   vits_neg_cent            the alignment scores of SynthesizerTrn.forward
+ *                            (models.py:483-490: exp, 2 matmuls, 2 sums)
  *   vits_conv1d_forward      nn.Conv1d / ConvTranspose1d forward of
  *                            modules.WN (modules.py:130-182),
  *                            modules.ResBlock2 (modules.py:250-260),
@@ -170,6 +172,16 @@ int vits_maximum_path_lengths(const float* neg_cent, const int32_t* t_t_len,
 /* bytes of workspace the two calls above need (0 when the backtrack bits */
 /* fit in LDS)                                                            */
 int64_t vits_maximum_path_workspace(int batch, int t_t, int t_s);
+
+/* ---------------------------------------------------------------------- */
+/* MAS scores (models.py:483-490): neg_cent[b][y][x] = sum_d(-0.5 log 2pi */
+/* - logs_p - 0.5 z_p^2 s + z_p m_p s - 0.5 m_p^2 s), s = exp(-2 logs_p). */
+/* z_p [B][C][t_t], m_p / logs_p [B][C][t_s], neg_cent [B][t_t][t_s], all */
+/* contiguous fp32.  Computed in fp32 over every (padded) position, as    */
+/* the reference does before its mask.                                    */
+/* ---------------------------------------------------------------------- */
+int vits_neg_cent(const float* z_p, const float* m_p, const float* logs_p, float* neg_cent,
+                  int batch, int channels, int t_t, int t_s, void* stream);
 
 /* ---------------------------------------------------------------------- */
 /* STFT magnitude and its adjoint.  x [B][L] fp32; the signal is reflect- */

@@ -318,3 +318,14 @@ def posterior_infer(sd: SD, spec, n, n_layers_q, H):
     C = stats.shape[1] // 2
     m, logs = stats[:, :C], stats[:, C:]
     return m + n * torch.exp(logs)
+
+
+def neg_cent(z_p, m_p, logs_p):
+    """MAS scores, models.py:483-489 (fp32, the four terms summed in the
+    reference's order)."""
+    s_p_sq_r = torch.exp(-2 * logs_p)
+    nc1 = torch.sum(-0.5 * math.log(2 * math.pi) - logs_p, [1], keepdim=True)
+    nc2 = torch.matmul(-0.5 * (z_p ** 2).transpose(1, 2), s_p_sq_r)
+    nc3 = torch.matmul(z_p.transpose(1, 2), (m_p * s_p_sq_r))
+    nc4 = torch.sum(-0.5 * (m_p ** 2) * s_p_sq_r, [1], keepdim=True)
+    return nc1 + nc2 + nc3 + nc4

@@ -264,3 +264,20 @@ def test_attention_fused_qkv_strides(device):
     out = torch.empty(B, H * D, T, device=device)
     engine._attention_into(qkv.to(device), H * D, H, None, out)
     _close(out, ref, tol=2e-5, what="fused-qkv attention")
+
+
+@pytest.mark.parametrize("B,C,Tt,Ts", [(3, 192, 500, 100), (2, 5, 37, 13), (1, 16, 1, 1), (2, 192, 129, 33)])
+def test_neg_cent(device, B, C, Tt, Ts):
+    """vits_neg_cent vs the models.py:483-489 formula in float64 (the HIP
+    kernel accumulates in fp32 in a different order: tol 2e-6 of max|nc|)."""
+    from oracle.vits_oracle import neg_cent as nc_ref
+
+    g = torch.Generator().manual_seed(B * 1000 + Tt)
+    z = torch.randn(B, C, Tt, generator=g)
+    m = torch.randn(B, C, Ts, generator=g)
+    lg = torch.randn(B, C, Ts, generator=g) * 0.5
+    ref = nc_ref(z.double(), m.double(), lg.double())
+    out = ops.neg_cent(z.to(device), m.to(device), lg.to(device))
+    assert out.shape == (B, Tt, Ts) and out.dtype == torch.float32
+    err = (out.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err

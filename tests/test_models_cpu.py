@@ -52,10 +52,17 @@ def _mas_oracle(neg_cent, mask):
     return torch.from_numpy(p).to(device=neg_cent.device, dtype=neg_cent.dtype)
 
 
+def _neg_cent_oracle(z_p, m_p, logs_p):
+    from oracle.vits_oracle import neg_cent
+
+    return neg_cent(z_p.detach().float(), m_p.detach().float(), logs_p.detach().float())
+
+
 def test_training_forward_matches_reference(monkeypatch):
     import vits_amd.models as vm
 
     monkeypatch.setattr(vm, "maximum_path", _mas_oracle)
+    monkeypatch.setattr(vm, "neg_cent_scores", _neg_cent_oracle)
     c = tiny_cfg()
     m = build_model(c["model"], c["data"])
     gd = golden("tiny_forward.npz")
@@ -80,6 +87,7 @@ def test_training_forward_backward_runs(monkeypatch):
     import vits_amd.models as vm
 
     monkeypatch.setattr(vm, "maximum_path", _mas_oracle)
+    monkeypatch.setattr(vm, "neg_cent_scores", _neg_cent_oracle)
     c = tiny_cfg()
     m = build_model(c["model"], c["data"]).train()
     gd = golden("tiny_forward.npz")

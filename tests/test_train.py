@@ -50,11 +50,18 @@ def _cpu_mas(neg_cent, mask):
     return torch.from_numpy(p).to(device=neg_cent.device, dtype=neg_cent.dtype)
 
 
+def _cpu_neg_cent(z_p, m_p, logs_p):
+    from oracle.vits_oracle import neg_cent
+
+    return neg_cent(z_p.detach().float(), m_p.detach().float(), logs_p.detach().float())
+
+
 def _patch_cpu():
     import vits_amd.models as vm
     import vits_amd.ops as ops
 
     vm.maximum_path = _cpu_mas
+    vm.neg_cent_scores = _cpu_neg_cent
     ops.stft_mag = _cpu_stft_mag
 
 
@@ -142,6 +149,7 @@ def test_train_step_cpu_reduces_loss_and_updates(monkeypatch):
     import vits_amd.ops as ops
 
     monkeypatch.setattr(vm, "maximum_path", _cpu_mas)
+    monkeypatch.setattr(vm, "neg_cent_scores", _cpu_neg_cent)
     monkeypatch.setattr(ops, "stft_mag", _cpu_stft_mag)
     hps = tiny_hps()
     st = _make(hps, torch.device("cpu"))

@@ -22,6 +22,8 @@ shapes.append(("up1", 256, 128, 12, 1, 8 * Ty, False, (6, 12)))
 shapes.append(("pre", 192, 512, 7, 1, Ty, False, None))
 
 only = os.environ.get("ONLY")
+tiles = [int(t) for t in os.environ.get("TILES", "").split(",") if t]
+kcms = [int(t) for t in os.environ.get("KCM", "1").split(",") if t]
 reps = int(os.environ.get("REPS", "5"))
 tot_fl, tot_ms = 0, 0
 res = {}
@@ -44,19 +46,41 @@ for name, cin, cout, k, d, T, gate, up in shapes:
         cond = torch.randn(B, cout, device=dev) if gate else None
         desc = make_desc(layer, x, make_out(y, res=res_t), in_slope=0.1, cond=cond)
         flops = 2 * B * cout * T * cin * k
-    for _ in range(2):
-        ops.conv1d_launch(desc, B, dev)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        ops.conv1d_launch(desc, B, dev)
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / reps
+    def timeit():
+        for _ in range(2):
+            ops.conv1d_launch(desc, B, dev)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            ops.conv1d_launch(desc, B, dev)
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps
+
+    ms = timeit()
+    alt = ""
+    if tiles:
+        t0, kc0 = desc.tile, desc.kc
+        for t in tiles:
+            if layer.m_pad % 128 == 0 and (t != 0 or layer.tile == 0):
+                best = None
+                for mlt in kcms:
+                    kc = kc0 * mlt
+                    if layer.cin_pad % kc:
+                        continue
+                    desc.tile, desc.kc = t, kc
+                    try:
+                        v = flops / timeit() / 1e9
+                    except Exception:  # noqa: BLE001
+                        continue
+                    if best is None or v > best[0]:
+                        best = (v, kc)
+                alt += f" t{t}=" + ("ERR" if best is None else f"{best[0]:6.1f}@{best[1]}")
+        desc.tile, desc.kc = t0, kc0
     tf = flops / ms / 1e9
     res[name] = round(tf, 1)
-    print(f"{name:18s} cin={cin:4d} cout={cout:4d} k={k:2d} d={d} T={T:6d} tile={layer.tile} kc={layer.kc}  {ms*1e3:8.1f} us  {tf:6.1f} TF/s", flush=True)
+    print(f"{name:18s} cin={cin:4d} cout={cout:4d} k={k:2d} d={d} T={T:6d} tile={layer.tile} kc={layer.kc}  {ms*1e3:8.1f} us  {tf:6.1f} TF/s{alt}", flush=True)
     tot_fl += flops
     tot_ms += ms
 print(f"TOTAL {tot_fl/tot_ms/1e9:.1f} TF/s over {tot_ms:.2f} ms")

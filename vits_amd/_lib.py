@@ -102,6 +102,11 @@ _SIGS = {
          C.c_void_p, C.c_int64, C.c_void_p],
     ),
     "vits_maximum_path_workspace": (C.c_int64, [C.c_int, C.c_int, C.c_int]),
+    "vits_neg_cent": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+         C.c_void_p],
+    ),
     "vits_stft_mag_forward": (
         C.c_int,
         [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,

@@ -26,6 +26,7 @@ from torch.nn.utils import remove_weight_norm, weight_norm
 from . import attentions, commons, engine, modules
 from .commons import gen_sin_table, get_padding, init_weights
 from .monotonic_align import maximum_path
+from .ops import neg_cent as neg_cent_scores
 
 
 def _needs_grad(module: nn.Module, *tensors) -> bool:
@@ -326,12 +327,9 @@ class SynthesizerTrn(nn.Module):
         z_p = self.flow(z, y_mask, g=g)
 
         with torch.no_grad():
-            s_p_sq_r = torch.exp(-2 * logs_p)
-            neg_cent1 = torch.sum(-0.5 * math.log(2 * math.pi) - logs_p, [1], keepdim=True)
-            neg_cent2 = torch.matmul(-0.5 * (z_p ** 2).transpose(1, 2), s_p_sq_r)
-            neg_cent3 = torch.matmul(z_p.transpose(1, 2), (m_p * s_p_sq_r))
-            neg_cent4 = torch.sum(-0.5 * (m_p ** 2) * s_p_sq_r, [1], keepdim=True)
-            neg_cent = neg_cent1 + neg_cent2 + neg_cent3 + neg_cent4
+            # one fp32 MFMA kernel for the exp / 2 matmuls / 2 sums of
+            # models.py:484-489 (vits_neg_cent)
+            neg_cent = neg_cent_scores(z_p, m_p, logs_p)
             if self.align_noise > 0:
                 eps = noise_align if noise_align is not None else torch.randn_like(neg_cent)
                 neg_cent = neg_cent + torch.std(neg_cent) * eps * self.align_noise

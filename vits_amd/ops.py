@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 from ._lib import (ACT_NONE, ConvDesc, ConvOut, EPI_GATE, EPI_STORE, EPI_UPSAMPLE, TILE_128x128,
-                   TILE_32x256, TILE_64x256, TILE_ROWS, check)
+                   TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS, check)
 
 # ---------------------------------------------------------------------------
 # plumbing
@@ -54,26 +54,45 @@ def weight_norm_effective(module: torch.nn.Module, name: str = "weight") -> torc
 # ---------------------------------------------------------------------------
 
 
-def _pick_tile(m: int) -> int:
+def _pick_tile(m: int, k: int) -> int:
+    """Workgroup tile by GEMM rows and taps, from the per-shape sweep of
+    tools/conv_bench.py on MI355X (B=16, Ty=500 decoder/flow shapes):
+    64x128 wins for k <= 7 (more workgroups, no half-empty last round on
+    4000-column grids: +5..25 %), 128x128 for the long k=11 reductions
+    (+5 %), 64x256 for 64-row k=7, 32x256 for 32 rows."""
     if m > 64:
-        return TILE_128x128
+        return TILE_128x128 if k >= 9 else TILE_64x128
     if m > 32:
-        return TILE_64x256
+        return TILE_64x256 if 5 <= k <= 8 else TILE_64x128
     return TILE_32x256
 
 
-TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, 3: 128}
+TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, TILE_64x128: 128}
 W_TILE_FLOATS = 4096                                   # conv1d.hip VITS_W_TILE
 X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::floats
+
+
+# workgroups per CU each tile reaches by its VGPR count (ISA dump of
+# conv1d.hip: 128x128 154 VGPRs -> 3 waves/SIMD, 64x256 / 32x256 ~122 -> 4,
+# 64x128 89 -> 5); the K-chunk is sized so that LDS does not cut this further
+TILE_OCCUPANCY = {TILE_128x128: 3, TILE_64x256: 4, TILE_32x256: 4, TILE_64x128: 5}
+LDS_BYTES_PER_CU = 160 * 1024
 
 
 def _pick_kc(cin: int, k: int, dil: int, tile: int) -> int:
     """Input channels per K-chunk: the largest even kc within the kernel's
     per-stage LDS/register budgets (W chunk kc*k*BM floats, X chunk
-    kc*xw_pad floats)."""
+    kc*xw_pad floats) AND within the LDS share that keeps the tile's VGPR
+    occupancy (the conv is latency-bound at small K: on MI355X a 64x128 k=3
+    conv runs 86 TF/s at kc=10 / 5 WGs per CU but 77 TF/s at kc=14 / 4)."""
     bm, bn = TILE_ROWS[tile], TILE_COLS[tile]
     xw_pad = (bn + (k - 1) * dil + 3) // 4 * 4
-    budget = min(32, W_TILE_FLOATS // (k * bm), X_TILE_FLOATS[bn] // xw_pad, cin + (cin & 1))
+    lds_fixed = 4 * (2 * k * bm + 2 * xw_pad + 64)
+    lds_floats = (LDS_BYTES_PER_CU // TILE_OCCUPANCY[tile] - lds_fixed) // 8  # per stage, W+X
+    occ_kc = lds_floats // (k * bm + xw_pad)
+    occ_kc = max(occ_kc, 2 * -(-12 // k))  # but keep >= ~24 taps x channels per chunk
+    budget = min(32, W_TILE_FLOATS // (k * bm), X_TILE_FLOATS[bn] // xw_pad, occ_kc,
+                 cin + (cin & 1))
     budget = max(2, budget - (budget & 1))
     # zero-padded channels cost MFMA work, each chunk costs a fixed overhead
     # (~2 channels' worth): minimise ceil(cin/kc) * (kc + 2)
@@ -136,7 +155,7 @@ def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], *, dilation: i
         epi, outc = EPI_GATE, h
     else:
         rows, epi, outc = w, EPI_STORE, cout
-    tile = _pick_tile(cout)
+    tile = _pick_tile(cout, k)
     packed, kc = _finish_pack(rows, k, tile, dilation)
     b = None if bias is None else bias.detach().to(torch.float32).contiguous()
     return PackedConv(packed, b, cin, cout, k, dilation, padding, epi, tile, kc,
@@ -157,7 +176,7 @@ def pack_conv_transpose(weight: torch.Tensor, bias: Optional[torch.Tensor], stri
     w4 = w.reshape(cin, cout, kp, u)
     # rows (o, r), taps j' = kp-1-i
     rows = w4.flip(2).permute(1, 3, 0, 2).reshape(cout * u, cin, kp)
-    tile = _pick_tile(cout * u)
+    tile = _pick_tile(cout * u, kp)
     packed, kc = _finish_pack(rows, kp, tile)
     b = None if bias is None else bias.detach().to(torch.float32).contiguous()
     return PackedConv(packed, b, cin, cout * u, kp, 1, kp - 1, EPI_UPSAMPLE, tile, kc,
@@ -423,6 +442,24 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, n_heads: int,
 
 _DT = {torch.float32: _lib.DT_F32, torch.float16: _lib.DT_F16, torch.bfloat16: _lib.DT_BF16,
        torch.int32: _lib.DT_I32}
+
+
+def neg_cent(z_p: torch.Tensor, m_p: torch.Tensor, logs_p: torch.Tensor) -> torch.Tensor:
+    """MAS scores [B, t_t, t_s] of models.py:483-490 in one fp32 MFMA kernel
+    (no autograd: the reference computes them under torch.no_grad)."""
+    require_device(z_p, m_p, logs_p)
+    z = z_p.detach().to(torch.float32).contiguous()
+    m = m_p.detach().to(torch.float32).contiguous()
+    lg = logs_p.detach().to(torch.float32).contiguous()
+    B, C, Tt = z.shape
+    if m.shape != lg.shape or m.shape[0] != B or m.shape[1] != C:
+        raise _lib.VitsAmdError(f"neg_cent: z_p {tuple(z.shape)} m_p {tuple(m.shape)} "
+                                f"logs_p {tuple(lg.shape)}")
+    Ts = m.shape[2]
+    out = torch.empty(B, Tt, Ts, device=z.device, dtype=torch.float32)
+    check(_lib.load().vits_neg_cent(z.data_ptr(), m.data_ptr(), lg.data_ptr(), out.data_ptr(),
+                                    B, C, Tt, Ts, _stream_ptr(z.device)), "vits_neg_cent")
+    return out
 
 
 def maximum_path(neg_cent: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
