@@ -18,6 +18,7 @@ Extra fields:
                 against the fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
   cpu_baseline  the CPU oracle (oracle/vits_oracle.py, torch fp32 CPU: the
                 reference algorithm restated) on a bounded sample.
+  longform      BASELINE C5 (30 s utterances, B=4, hipGraph replay).
   train         the metric's second half (BASELINE configs 3/4): train utt/s of
                 the train_stft step (vits_amd/train.py: G fwd/bwd, MWSD D,
                 HIP MAS + MR-STFT, fp16 autocast, AdamW/RAdam) at
@@ -28,6 +29,7 @@ Extra fields:
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
        [--tx 100] [--ty 500] [--graph] [--no-cpu-baseline]
        [--train-batch 32] [--train-steps 5] [--train-warmup 2] [--no-train]
+       [--no-longform]
 """
 from __future__ import annotations
 
@@ -119,6 +121,31 @@ def pmc_traffic():
     return c.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def longform_leg(model, device, rank, steps=5, warmup=2, B=4, Tx=500, Ty=2500):
+    """BASELINE C5: 30 s utterances (B=4, Tx=500, Ty=2500 -> 480,000 samples
+    each), the whole infer_p2 replayed from one captured hipGraph."""
+    inputs = make_inputs(B, Tx, Ty, device, seed=4321 + rank)
+    with torch.no_grad():
+        run = model.capture_infer_p2(B, Tx, Ty)
+        for _ in range(warmup):
+            run(*inputs)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run(*inputs)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    samples = steps * B * Ty * HOP
+    del run
+    torch.cuda.empty_cache()
+    return {"value": round(samples / el, 1), "unit": "output samples/s",
+            "ms_per_step": round(el / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "x_realtime_22k": round(samples / el / 22050.0, 1), "dtype": "fp32",
+            "workload": f"infer_p2 batch={B} Tx={Tx} Ty={Ty} ({Ty * HOP / SR:.0f} s @16 kHz), "
+                        "whole step replayed from one hipGraph",
+            "note": "C5 asks bf16; this line is the fp32 kernels (a bf16 conv path is not built yet)"}
+
+
 def train_leg(args, device, rank, world, dist):
     """Timed train_stft steps (BASELINE C3/C4) on synthetic base.json batches."""
     from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
@@ -177,6 +204,7 @@ def main():
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--train-warmup", type=int, default=2)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--no-longform", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +217,10 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank)
     device = torch.device("cuda", local_rank)
+
+    # the train leg runs first, on a clean allocator (its MIOpen algorithm
+    # choice depends on free workspace), and releases its memory afterwards
+    train = None if args.no_train else train_leg(args, device, rank, world, dist)
 
     model = build_model(device)
     B, Tx, Ty = args.batch, args.tx, args.ty
@@ -237,7 +269,7 @@ def main():
                     "flops_per_launch": int(per_launch_flops),
                     "conv_ms_per_step": round(s["total_ms"] / args.steps, 3)}
 
-    train = None if args.no_train else train_leg(args, device, rank, world, dist)
+    longform = None if args.no_longform else longform_leg(model, device, rank)
 
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if dist:
@@ -264,6 +296,7 @@ def main():
             "rtf_16k": round((ms_per_step / 1e3) / (B * Ty * HOP / SR), 6),
             "x_realtime_22k": round(value / world / 22050.0, 1),
             "roofline": roof,
+            "longform": longform,
             "train": train,
         }
         if not args.no_cpu_baseline and world == 1:

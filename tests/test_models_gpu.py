@@ -165,3 +165,61 @@ def test_training_forward_gpu_vs_reference(device):
     assert torch.equal(ids_slice.cpu(), t["ids_slice"])
     assert rel_err(o.detach(), gd["o"]) < 1e-4
     assert rel_err(out[7].detach(), gd["z_q"]) < 1e-4
+
+
+# --------------------------------------------------------------------------
+# module-level parity (base.json shapes, deterministic weights) vs the oracle
+# --------------------------------------------------------------------------
+
+def test_posterior_infer_vs_oracle(base, device):
+    from oracle import vits_oracle as V
+
+    g = torch.Generator().manual_seed(7)
+    spec = torch.rand(2, 513, 123, generator=g)
+    n = torch.randn(2, 192, 123, generator=g)
+    got = base.enc_q.infer(spec.to(device), n.to(device))
+    ref = V.posterior_infer(oracle_sd(base), spec, n, BASE_MODEL["n_layers_q"], 256)
+    assert rel_err(got, ref) < REL
+
+
+def test_wn_infer_vs_oracle(base, device):
+    """The flow's WN (cond from g, 4 layers, unmasked infer)."""
+    from oracle import vits_oracle as V
+
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(2, 256, 77, generator=g) * 0.5
+    gg = torch.randn(2, 1024, generator=g) * 0.5
+    wn = base.flow.flows[0].enc
+    got = wn.infer(x.to(device), gg.to(device))
+    ref = V.wn(oracle_sd(base), "flow.flows.0.enc", x, None, gg, 4, 256, masked=False)
+    assert rel_err(got, ref) < REL
+
+
+@pytest.mark.parametrize("idx", [0, 4, 8, 11])
+def test_resblock2_vs_oracle(base, device, idx):
+    """ResBlock2 no-grad path (fused HIP convs) for the k=3/7/11 blocks of
+    stages 0..3 (C=256..32)."""
+    from oracle import vits_oracle as V
+
+    rb = base.dec.resblocks[idx]
+    C = rb.convs1[0].in_channels
+    g = torch.Generator().manual_seed(idx)
+    x = torch.randn(2, C, 301, generator=g) * 0.5
+    gg = torch.randn(2, 1024, generator=g) * 0.5
+    with torch.no_grad():
+        got = rb(x.to(device), gg.to(device))
+    ref = V.resblock2(oracle_sd(base), f"dec.resblocks.{idx}", x, gg, rb.kernel_size, rb.dilation)
+    assert rel_err(got, ref) < REL
+
+
+def test_generator_vs_oracle(base, device):
+    from oracle import vits_oracle as V
+
+    g = torch.Generator().manual_seed(9)
+    z = torch.randn(2, 192, 37, generator=g) * 0.7
+    gg = torch.randn(2, 1024, generator=g) * 0.5
+    with torch.no_grad():
+        got = base.dec(z.to(device), gg.to(device))
+    ref = V.generator(oracle_sd(base), z, gg, BASE_MODEL)
+    assert got.shape == ref.shape == (2, 1, 37 * 192)
+    assert snr_db(got, ref) >= SNR_DB and rel_err(got, ref) < REL

@@ -21,13 +21,14 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-mels", action="store_true")
+    ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--torch-prof", default=None, help="write a torch.profiler op table here")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     hps = default_hps()
     torch.manual_seed(1234)
     g, d = build_models(hps, dev)
-    st = TrainStep(hps, g, d, dev, log_mels=not args.no_mels)
+    st = TrainStep(hps, g, d, dev, log_mels=not args.no_mels, fused_adamw=not args.no_fused)
     batch = [t.to(dev) for t in synthetic_batch(hps, args.batch, seed=0)]
     for i in range(args.warmup):
         t0 = time.perf_counter()

@@ -45,14 +45,15 @@ def build_models(hps, device):
 
 
 class TrainStep:
-    def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True):
+    def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True, fused_adamw=True):
         self.hps = hps
         self.device = device
         self.log_mels = log_mels
         self.mstft = MultiResolutionSTFTLoss().to(device)
         self.optim_g = torch.optim.AdamW(net_g.parameters(), hps.train.learning_rate,
                                          betas=hps.train.betas, weight_decay=hps.train.weight_decay,
-                                         eps=hps.train.eps, fused=device.type == "cuda")
+                                         eps=hps.train.eps,
+                                         fused=fused_adamw and device.type == "cuda")
         self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4)
         if ddp:
             ids = [device.index] if device.type == "cuda" else None
