@@ -159,27 +159,34 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
       }
     }
   };
-  // ---- X chunk: global -> registers (zero padding + leaky-relu prologue) ------
+  // ---- X chunk: global -> registers, raw.  Every lane issues its loads
+  // unconditionally (padding lanes read the batch's first element) so the
+  // compiler cannot tie a wait to each load: all MAXX loads stay in flight
+  // under the chunk's MFMAs and are consumed in lstore.
   auto gload = [&](int c0) {
     const float* base = xb + (int64_t)c0 * p.x_cstride;
     const int lim = p.cin - c0;  // rows >= lim are channel padding
 #pragma unroll
     for (int q = 0; q < MAXX; ++q) {
-      float v = 0.f;
-      if (xrow[q] < lim) {
-        v = base[xoff[q]];
-        if (act_in) v = v < 0.f ? v * slope : v;
+      if (q * 256 < xsz) {  // workgroup-uniform: no exec-mask branch
+        const bool ok = xrow[q] < lim;
+        xreg[q] = *(ok ? base + xoff[q] : xb);
       }
-      xreg[q] = v;
     }
   };
-  // ---- registers -> LDS stage ------------------------------------------------
-  auto lstore = [&](float* st) {
+  // ---- registers -> LDS stage (zero padding + leaky-relu prologue) -----------
+  auto lstore = [&](float* st, int c0) {
     float* xs = st + wsz;
+    const int lim = p.cin - c0;
 #pragma unroll
     for (int q = 0; q < MAXX; ++q) {
-      const int i = tid + q * 256;
-      if (i < xsz) xs[i] = xreg[q];
+      if (q * 256 < xsz) {
+        const int i = tid + q * 256;
+        float v = xreg[q];
+        if (act_in) v = v < 0.f ? v * slope : v;
+        v = xrow[q] < lim ? v : 0.f;
+        if (i < xsz) xs[i] = v;
+      }
     }
   };
 
@@ -189,7 +196,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 
   wdma(0, stage0);
   gload(0);
-  lstore(stage0);
+  lstore(stage0, 0);
   __syncthreads();
 
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
         for (int ni = 0; ni < TN; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
     }
-    if (more) lstore(nxt);
+    if (more) lstore(nxt, (ch + 1) * kc);
     __syncthreads();
   }
 
@@ -272,35 +279,44 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   OutDesc o0{p.out0.y, p.out0.y_bstride, p.out0.y_cstride, p.out0.act, p.out0.res,
              p.out0.res_bstride, p.out0.res_cstride, p.out0.res_scale, p.out0.accumulate,
              p.out0.post_div};
+  // per-row additive constant (bias + per-utterance cond) of this tile's BM
+  // rows, fetched once by BM threads in parallel into LDS (the stages are
+  // free after the last barrier of the K loop)
+  float* const erow = smem;
+  if (tid < BM) {
+    const int row = m0 + tid;
+    float e = 0.f;
+    if (row < p.m) {
+      int idx = row;
+      if (EPI == VITS_EPI_GATE) idx = (row & 1) ? (p.m >> 1) + (row >> 1) : (row >> 1);
+      if (EPI == VITS_EPI_UPSAMPLE) idx = row / p.up_u;
+      if (p.bias) e = p.bias[idx];
+      if (cond && EPI != VITS_EPI_UPSAMPLE) e += cond[idx];
+    }
+    erow[tid] = e;
+  }
+  __syncthreads();
 
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = n0 + wn + ni * 32 + l32;
-      const int rbase = m0 + wm + mi * 32 + 4 * lhi;
+      const int rloc = wm + mi * 32 + 4 * lhi;  // tile-local row of register 0
+      const int rbase = m0 + rloc;
       if (EPI == VITS_EPI_GATE) {
         // packed rows 2q (tanh half) / 2q+1 (sigmoid half) live in the same
         // lane in registers r, r+1 (r even): no cross-lane traffic.
-        const int H = p.m >> 1;
         if (n < p.n_out) {
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
-            const int row = rbase + (r & 3) + 8 * (r >> 2);
+            const int ro = (r & 3) + 8 * (r >> 2);
+            const int row = rbase + ro;
             if (row < p.m) {
-              const int q = row >> 1;
-              float va = acc[mi][ni][r];
-              float vb = acc[mi][ni][r + 1];
-              if (p.bias) {
-                va += p.bias[q];
-                vb += p.bias[H + q];
-              }
-              if (cond) {
-                va += cond[q];
-                vb += cond[H + q];
-              }
-              float v = fast_tanh(va) * fast_sigmoid(vb);
-              store_std(o0, b, q, n, v, n >= len_b);
+              const float va = acc[mi][ni][r] + erow[rloc + ro];
+              const float vb = acc[mi][ni][r + 1] + erow[rloc + ro + 1];
+              const float v = fast_tanh(va) * fast_sigmoid(vb);
+              store_std(o0, b, row >> 1, n, v, n >= len_b);
             }
           }
         }
@@ -308,14 +324,14 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
         const int u = p.up_u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = rbase + (r & 3) + 8 * (r >> 2);
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const int row = rbase + ro;
           if (row < p.m && n < p.n_out) {
             const int oc = row / u;
             const int ph = row - oc * u;
             const int t = n * u + ph - p.up_pad;
             if (t >= 0 && t < p.t_out) {
-              float v = acc[mi][ni][r];
-              if (p.bias) v += p.bias[oc];
+              const float v = acc[mi][ni][r] + erow[rloc + ro];
               store_std(o0, b, oc, t, v, t >= len_b);
             }
           }
@@ -327,11 +343,10 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
         if (n < p.n_out) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int row = rbase + (r & 3) + 8 * (r >> 2);
+            const int ro = (r & 3) + 8 * (r >> 2);
+            const int row = rbase + ro;
             if (row < p.m) {
-              float v = acc[mi][ni][r];
-              if (p.bias) v += p.bias[row];
-              if (cond) v += cond[row];
+              const float v = acc[mi][ni][r] + erow[rloc + ro];
               if (row < p.split)
                 store_std(o0, b, row, n, v, n >= len_b);
               else
@@ -347,14 +362,8 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
         if (n < p.n_out) {
           float v[16];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = rbase + (r & 3) + 8 * (r >> 2);
-            const bool ok = row < p.m;
-            float t = acc[mi][ni][r];
-            if (p.bias) t += ok ? p.bias[row] : 0.f;
-            if (cond) t += ok ? cond[row] : 0.f;
-            v[r] = apply_act(t, o0.act);
-          }
+          for (int r = 0; r < 16; ++r)
+            v[r] = apply_act(acc[mi][ni][r] + erow[rloc + (r & 3) + 8 * (r >> 2)], o0.act);
           float* yb = o0.y + (int64_t)b * o0.y_bstride + n;
           if (o0.res) {
             const float* rb = o0.res + (int64_t)b * o0.res_bstride + n;
@@ -362,7 +371,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              rv[r] = row < p.m ? rb[(int64_t)row * o0.res_cstride] : 0.f;
+              rv[r] = rb[(int64_t)(row < p.m ? row : 0) * o0.res_cstride];
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = rv[r] + o0.res_scale * v[r];
@@ -372,7 +381,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              yo[r] = row < p.m ? yb[(int64_t)row * o0.y_cstride] : 0.f;
+              yo[r] = yb[(int64_t)(row < p.m ? row : 0) * o0.y_cstride];
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = yo[r] + v[r];
