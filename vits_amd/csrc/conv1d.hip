@@ -462,8 +462,15 @@ int conv1d_one(const vits_conv1d_desc& d, int batch, hipStream_t s) {
     }
     case VITS_TILE_64x128:
       return launch_tile<64, 128, 2, 2>(d, batch, s);
-    case VITS_TILE_64x256:
+    case VITS_TILE_64x256: {
+      // same fallback for 64x256 grids (the flow / text-side convs at
+      // T ~ 500) when the chunk's input window also fits the 128-column tile
+      const long blocks = (long)((d.n_out + 255) / 256) * ((d.m + 63) / 64) * batch;
+      const int xw_pad128 = (128 + (d.k - 1) * d.dil + 3) & ~3;
+      if (blocks < 512 && d.kc * xw_pad128 <= XTile<128>::floats)
+        return launch_tile<64, 128, 2, 2>(d, batch, s);
       return launch_tile<64, 256, 1, 4>(d, batch, s);
+    }
     case VITS_TILE_32x256:
       return launch_tile<32, 256, 1, 4>(d, batch, s);
     default:

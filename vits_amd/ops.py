@@ -57,14 +57,17 @@ def weight_norm_effective(module: torch.nn.Module, name: str = "weight") -> torc
 def _pick_tile(m: int, k: int) -> int:
     """Workgroup tile by GEMM rows and taps, from the per-shape sweep of
     tools/conv_bench.py on MI355X (B=16, Ty=500 decoder/flow shapes):
-    64x128 wins for k <= 7 (more workgroups, no half-empty last round on
-    4000-column grids: +5..25 %), 128x128 for the long k=11 reductions
-    (+5 %), 64x256 for 64-row k=7, 32x256 for 32 rows."""
-    if m > 64:
-        return TILE_128x128 if k >= 9 else TILE_64x128
-    if m > 32:
-        return TILE_64x256 if 5 <= k <= 8 else TILE_64x128
-    return TILE_32x256
+    32 rows -> 32x256; k <= 4 (k=3 resblock convs, 2-tap polyphase ups,
+    1x1) -> 64x128; k = 5..9 and 64/128-row k=11 -> 64x256; k=11 with
+    more rows -> 128x128.  Grids too small to fill the chip twice fall back
+    to 64x128 at launch (conv1d.hip)."""
+    if m <= 32:
+        return TILE_32x256
+    if k <= 4:
+        return TILE_64x128
+    if k <= 9 or m <= 128:
+        return TILE_64x256
+    return TILE_128x128
 
 
 TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, TILE_64x128: 128}
@@ -74,8 +77,9 @@ X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::
 
 # workgroups per CU each tile reaches by its VGPR count (ISA dump of
 # conv1d.hip: 128x128 154 VGPRs -> 3 waves/SIMD, 64x256 / 32x256 ~122 -> 4,
-# 64x128 89 -> 5); the K-chunk is sized so that LDS does not cut this further
-TILE_OCCUPANCY = {TILE_128x128: 3, TILE_64x256: 4, TILE_32x256: 4, TILE_64x128: 5}
+# 64x128 89 -> 5; 64x256 is budgeted at 3: its k=7 convs run faster with the
+# bigger chunk); the K-chunk is sized so that LDS does not cut this further
+TILE_OCCUPANCY = {TILE_128x128: 3, TILE_64x256: 3, TILE_32x256: 4, TILE_64x128: 5}
 LDS_BYTES_PER_CU = 160 * 1024
 
 
