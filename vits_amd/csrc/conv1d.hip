@@ -68,11 +68,15 @@ constexpr int VITS_W_TILE = 4096;
 // owned by thread i % 256; its (row, column) -> global offset mapping does
 // not depend on the chunk, so it is computed once per workgroup.  The host
 // keeps kc * xw_pad <= floats.
-template <int BN>
+template <int BN, bool BF = false>
 struct XTile {
-  static constexpr int floats = BN <= 128 ? 2048 : 4096;
+  // bf16-MFMA chunks carry >= 16 channels: a wider window budget
+  static constexpr int floats = BF ? (BN <= 128 ? 3072 : 5120) : (BN <= 128 ? 2048 : 4096);
   static constexpr int regs = floats / 256;
 };
+// bf16 W stage budget in float slots (2 bf16 each): k=11, kc=16, BM=64 fits
+constexpr int VITS_W_TILE_BF = 6144;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_void_t;
 
 __device__ __forceinline__ float fast_sigmoid(float x) {
@@ -83,7 +87,7 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool BF>
 __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_desc p) {
   constexpr int WM = BM / WAVES_M;
   constexpr int WN = BN / WAVES_N;
@@ -99,11 +103,15 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   const int xw = BN + (k - 1) * dil;
   const int xw_pad = (xw + 3) & ~3;
   const int wrows = kc * k;
-  const int wsz = wrows * BM;
-  const int xsz = kc * xw_pad;
+  const int wsz = BF ? wrows * BM / 2 : wrows * BM;  // W stage in float slots
+  const int xsz = kc * xw_pad;  // staged window elements
+  // bf16 path: the window sits in LDS as bf16 [t][kc + 4] (channel-contiguous
+  // per time step, 8-byte aligned rows) so a B fragment is two ds_read_b64
+  const int kcp = kc + 4;
+  const int xslots = BF ? (xw_pad * kcp + 1) / 2 : xsz;  // LDS float slots
   // two stages: [W0][X0][W1][X1]
   float* const stage0 = smem;
-  float* const stage1 = smem + wsz + xsz;
+  float* const stage1 = smem + wsz + xslots;
 
   const int b = blockIdx.z;
   const int n0 = blockIdx.x * BN;
@@ -129,7 +137,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   const int xstart = n0 - p.pad_left;
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
-  constexpr int MAXX = XTile<BN>::regs;
+  constexpr int MAXX = XTile<BN, BF>::regs;
   float xreg[MAXX];
   int xrow[MAXX];  // window row of element tid + 256q (1<<24 when it is padding)
   int xoff[MAXX];  // its global offset relative to row 0 of the chunk
@@ -147,14 +155,20 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   // ---- W chunk: LDS-DMA, one 1 KiB piece (256 floats) per wave instruction;
   // lane l of piece q lands at LDS float q*256 + 4l (lane-linear image)
   auto wdma = [&](int c0, float* st) {
-    const float* wsrc = p.w + (int64_t)c0 * k * p.m_pad + m0;
+    // the chunk's W image is R rows of L float slots, HBM row stride S:
+    //   f32:  [kc*k][BM] rows of W[c][j][m0..m0+BM)
+    //   bf16: [k*kc/8][BM*8 bf16] rows of W[chunk][j][c8][m0..m0+BM][8]
+    const int L = BF ? BM * 4 : BM;
+    const float* wsrc = BF ? p.w + ((int64_t)(c0 / kc) * (k * (kc / 8)) * p.m_pad + m0) * 4
+                           : p.w + (int64_t)c0 * k * p.m_pad + m0;
+    const int64_t S = BF ? (int64_t)p.m_pad * 4 : p.m_pad;
     const int pieces = (wsz + 255) >> 8;
     for (int q = wid; q < pieces; q += 4) {
       const int e = q * 256 + lane * 4;
       if (e < wsz) {
-        const int r = e / BM;
-        const int col = e - r * BM;
-        __builtin_amdgcn_global_load_lds(wsrc + (int64_t)r * p.m_pad + col,
+        const int r = e / L;
+        const int col = e - r * L;
+        __builtin_amdgcn_global_load_lds(wsrc + (int64_t)r * S + col,
                                          (lds_void_t)(st + q * 256), 16, 0, 0);
       }
     }
@@ -185,7 +199,15 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
         float v = xreg[q];
         if (act_in) v = v < 0.f ? v * slope : v;
         v = xrow[q] < lim ? v : 0.f;
-        if (i < xsz) xs[i] = v;
+        if (i < xsz) {
+          if constexpr (BF) {
+            const int r = i / xw_pad;
+            const int t = i - r * xw_pad;
+            reinterpret_cast<__bf16*>(xs)[t * kcp + r] = (__bf16)v;
+          } else {
+            xs[i] = v;
+          }
+        }
       }
     }
   };
@@ -210,64 +232,95 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 
     const float* ws = cur;
     const float* xs = cur + wsz;
-    // k-step s = (tap j, channel pair cp), cp fastest: A rows (2cp + lhi)*k + j
-    // of W, B row 2cp + lhi of X shifted by j*dil.  Two register sets ping-
-    // pong so the LDS reads of step s+1 are in flight under the MFMAs of s;
-    // the read after the last step runs past the chunk into padded LDS and
-    // is never consumed.
-    const float* wa = ws + lhi * k * BM + wm + l32;
-    const float* xa = xs + lhi * xw_pad + wn + l32;
-    const int sa = 2 * k * BM;
-    const int sb = 2 * xw_pad;
-    int j = 0, cp = 0;
-    const float* pa = wa;
-    const float* pb = xa;
-    auto advance = [&]() {
-      ++cp;
-      pa += sa;
-      pb += sb;
-      if (cp == half) {
-        cp = 0;
-        ++j;
-        pa = wa + j * BM;
-        pb = xa + j * dil;
+    if constexpr (BF) {
+      // k-step = (tap j, 16 channels): A = one 16-byte bf16x8 read per
+      // 32-row fragment (W image [j][c8][row][8]); B = 8 channel rows of the
+      // fp32 X window at column n + j*dil, rounded to bf16 in registers
+      const char* wbytes = reinterpret_cast<const char*>(ws);
+      const int c8n = kc >> 3;
+      for (int j = 0; j < k; ++j) {
+        for (int g = 0; g < (kc >> 4); ++g) {
+          bf16x8 a[TM], bb[TN];
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi)
+            a[mi] = *reinterpret_cast<const bf16x8*>(
+                wbytes + ((int64_t)((j * c8n + 2 * g + lhi) * BM + wm + mi * 32 + l32) << 4));
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) {
+            const __bf16* xp = reinterpret_cast<const __bf16*>(xs) +
+                               (wn + ni * 32 + l32 + j * dil) * kcp + 16 * g + 8 * lhi;
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(xp);
+            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(xp + 4);
+            bb[ni] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
+        }
       }
-    };
-    float a0[TM], b0[TN], a1[TM], b1[TN];
-#pragma unroll
-    for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
-    advance();
-    int s = 0;
-    for (; s + 2 <= steps; s += 2) {
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) a1[mi] = pa[mi * 32];
-#pragma unroll
-      for (int ni = 0; ni < TN; ++ni) b1[ni] = pb[ni * 32];
-      advance();
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
-#pragma unroll
+    } else {
+      // k-step s = (tap j, channel pair cp), cp fastest: A rows (2cp + lhi)*k + j
+      // of W, B row 2cp + lhi of X shifted by j*dil.  Two register sets ping-
+      // pong so the LDS reads of step s+1 are in flight under the MFMAs of s;
+      // the read after the last step runs past the chunk into padded LDS and
+      // is never consumed.
+      const float* wa = ws + lhi * k * BM + wm + l32;
+      const float* xa = xs + lhi * xw_pad + wn + l32;
+      const int sa = 2 * k * BM;
+      const int sb = 2 * xw_pad;
+      int j = 0, cp = 0;
+      const float* pa = wa;
+      const float* pb = xa;
+      auto advance = [&]() {
+        ++cp;
+        pa += sa;
+        pb += sb;
+        if (cp == half) {
+          cp = 0;
+          ++j;
+          pa = wa + j * BM;
+          pb = xa + j * dil;
+        }
+      };
+      float a0[TM], b0[TN], a1[TM], b1[TN];
+  #pragma unroll
       for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
-#pragma unroll
+  #pragma unroll
       for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
       advance();
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[mi], b1[ni], acc[mi][ni], 0, 0, 0);
-    }
-    if (s < steps) {
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+      int s = 0;
+      for (; s + 2 <= steps; s += 2) {
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi) a1[mi] = pa[mi * 32];
+  #pragma unroll
+        for (int ni = 0; ni < TN; ++ni) b1[ni] = pb[ni * 32];
+        advance();
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+  #pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
+  #pragma unroll
+        for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
+        advance();
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+  #pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[mi], b1[ni], acc[mi][ni], 0, 0, 0);
+      }
+      if (s < steps) {
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+  #pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+      }
     }
     if (more) lstore(nxt, (ch + 1) * kc);
     __syncthreads();
@@ -401,32 +454,34 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   }
 }
 
-template <int BM, int BN, int WM_, int WN_>
+template <int BM, int BN, int WM_, int WN_, bool BF>
 int launch_tile(const vits_conv1d_desc& d, int batch, hipStream_t s) {
   const int halo = (d.k - 1) * d.dil;
   const int xw_pad = (BN + halo + 3) & ~3;
-  const size_t wsz = (size_t)d.kc * d.k * BM;
+  const size_t wsz = BF ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
   const size_t xsz = (size_t)d.kc * xw_pad;
-  if (wsz > (size_t)VITS_W_TILE || xsz > (size_t)XTile<BN>::floats) return VITS_E_UNSUP;
+  if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) || xsz > (size_t)XTile<BN, BF>::floats)
+    return VITS_E_UNSUP;
+  const size_t xslots = BF ? ((size_t)xw_pad * (d.kc + 4) + 1) / 2 : xsz;
   // 32-bit window offsets
   if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
     return VITS_E_UNSUP;
   // + tail pad: the software pipeline reads one k-step past the last chunk
-  const size_t lds = sizeof(float) * (2 * (wsz + xsz) + 2 * (size_t)d.k * BM + 2 * xw_pad + 64);
+  const size_t lds = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xw_pad + 64);
   dim3 grid((d.n_out + BN - 1) / BN, (d.m + BM - 1) / BM, batch);
   dim3 block(256);
   switch (d.epi) {
     case VITS_EPI_STORE:
       if (d.split < d.m)
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2>), grid, block, lds, s, d);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, BF>), grid, block, lds, s, d);
       else
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE>), grid, block, lds, s, d);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, BF>), grid, block, lds, s, d);
       break;
     case VITS_EPI_GATE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE>), grid, block, lds, s, d);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, BF>), grid, block, lds, s, d);
       break;
     case VITS_EPI_UPSAMPLE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE>), grid, block, lds, s, d);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, BF>), grid, block, lds, s, d);
       break;
     default:
       return VITS_E_UNSUP;
@@ -445,37 +500,45 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   if (d.epi == VITS_EPI_UPSAMPLE) VITS_CHECK_SHAPE(d.up_u > 0 && d.m % d.up_u == 0 && d.t_out > 0);
   if (d.epi == VITS_EPI_STORE && d.split < d.m) VITS_CHECK_ARG(d.out1.y != nullptr);
   if ((reinterpret_cast<uintptr_t>(d.w) & 15) != 0) return VITS_E_SHAPE;
+  VITS_CHECK_ARG(d.wdtype == VITS_WDT_F32 || d.wdtype == VITS_WDT_BF16);
+  if (d.wdtype == VITS_WDT_BF16) VITS_CHECK_SHAPE((d.kc % 16) == 0);
   return VITS_OK;
 }
 
-int conv1d_one(const vits_conv1d_desc& d, int batch, hipStream_t s) {
-  int rc = check_desc(d, batch);
-  if (rc) return rc;
+template <bool BF>
+int conv1d_dispatch(const vits_conv1d_desc& d, int batch, hipStream_t s) {
   switch (d.tile) {
     case VITS_TILE_128x128: {
       // a 128x128 grid that cannot fill the chip twice over (256 CUs) runs
       // as 64x128 tiles: same packing (its W/X budgets are a subset), twice
       // the workgroups
       const long blocks = (long)((d.n_out + 127) / 128) * ((d.m + 127) / 128) * batch;
-      if (blocks < 512) return launch_tile<64, 128, 2, 2>(d, batch, s);
-      return launch_tile<128, 128, 2, 2>(d, batch, s);
+      if (blocks < 512) return launch_tile<64, 128, 2, 2, BF>(d, batch, s);
+      return launch_tile<128, 128, 2, 2, BF>(d, batch, s);
     }
     case VITS_TILE_64x128:
-      return launch_tile<64, 128, 2, 2>(d, batch, s);
+      return launch_tile<64, 128, 2, 2, BF>(d, batch, s);
     case VITS_TILE_64x256: {
       // same fallback for 64x256 grids (the flow / text-side convs at
       // T ~ 500) when the chunk's input window also fits the 128-column tile
       const long blocks = (long)((d.n_out + 255) / 256) * ((d.m + 63) / 64) * batch;
       const int xw_pad128 = (128 + (d.k - 1) * d.dil + 3) & ~3;
-      if (blocks < 512 && d.kc * xw_pad128 <= XTile<128>::floats)
-        return launch_tile<64, 128, 2, 2>(d, batch, s);
-      return launch_tile<64, 256, 1, 4>(d, batch, s);
+      if (blocks < 512 && d.kc * xw_pad128 <= XTile<128, BF>::floats)
+        return launch_tile<64, 128, 2, 2, BF>(d, batch, s);
+      return launch_tile<64, 256, 1, 4, BF>(d, batch, s);
     }
     case VITS_TILE_32x256:
-      return launch_tile<32, 256, 1, 4>(d, batch, s);
+      return launch_tile<32, 256, 1, 4, BF>(d, batch, s);
     default:
       return VITS_E_UNSUP;
   }
+}
+
+int conv1d_one(const vits_conv1d_desc& d, int batch, hipStream_t s) {
+  int rc = check_desc(d, batch);
+  if (rc) return rc;
+  return d.wdtype == VITS_WDT_BF16 ? conv1d_dispatch<true>(d, batch, s)
+                                   : conv1d_dispatch<false>(d, batch, s);
 }
 
 }  // namespace

@@ -50,7 +50,10 @@ def get_plan(module: torch.nn.Module, builder):
     sig = _param_signature(module)
     plan = module.__dict__.get(_PLAN_ATTR)
     if plan is None or plan.signature != sig:
-        with torch.no_grad():
+        # a bf16 model runs its convs on the bf16-MFMA kernel variant (fp32
+        # activations, fp32 accumulation); fp32 and fp16 models run exact fp32
+        lowp = sig[0] is not None and sig[0][2] == torch.bfloat16
+        with torch.no_grad(), ops.pack_bf16(lowp):
             plan = builder(module)
         plan.signature = sig
         module.__dict__[_PLAN_ATTR] = plan

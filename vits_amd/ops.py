@@ -7,15 +7,18 @@ Weight packing helpers turn reference-layout conv weights into the
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import threading
 from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, ConvDesc, ConvOut, EPI_GATE, EPI_STORE, EPI_UPSAMPLE, TILE_128x128,
-                   TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS, check)
+from ._lib import (ACT_NONE, WDT_BF16, WDT_F32, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
+                   EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS,
+                   check)
 
 # ---------------------------------------------------------------------------
 # plumbing
@@ -123,14 +126,15 @@ class PackedConv:
     up_pad: int = 0
     out_channels: int = 0      # channels of the produced tensor
     extra: dict = field(default_factory=dict)
+    wdtype: int = WDT_F32      # WDT_BF16: w is [cin_pad/kc][k][kc/8][m_pad][8] bf16
 
     @property
     def m_pad(self) -> int:
-        return self.w.shape[2]
+        return self.w.shape[3] if self.wdtype == WDT_BF16 else self.w.shape[2]
 
     @property
     def cin_pad(self) -> int:
-        return self.w.shape[0]
+        return self.w.shape[0] * self.kc if self.wdtype == WDT_BF16 else self.w.shape[0]
 
 
 def _finish_pack(rows_w: torch.Tensor, k: int, tile: int, dil: int = 1) -> tuple[torch.Tensor, int]:
@@ -142,6 +146,44 @@ def _finish_pack(rows_w: torch.Tensor, k: int, tile: int, dil: int = 1) -> tuple
     packed = rows_w.new_zeros(cin_pad, k, m_pad, dtype=torch.float32)
     packed[:cin, :, :m] = rows_w.permute(1, 2, 0).to(torch.float32)
     return packed.contiguous(), kc
+
+
+class _PackPrecision(threading.local):
+    bf16 = False
+
+
+PACK_PRECISION = _PackPrecision()
+
+
+@contextlib.contextmanager
+def pack_bf16(enabled: bool = True):
+    """While active, pack_conv / pack_conv_transpose return bf16-MFMA layers
+    (engine plans of a bf16 model are built under it)."""
+    old = PACK_PRECISION.bf16
+    PACK_PRECISION.bf16 = bool(enabled)
+    try:
+        yield
+    finally:
+        PACK_PRECISION.bf16 = old
+
+
+def to_bf16(layer: PackedConv) -> PackedConv:
+    """Re-pack an fp32 layer for the bf16-MFMA kernel variant: K-chunks of 16
+    channels, W as [cin_pad/16][k][2][m_pad][8] bf16 (one 16-byte A fragment
+    per row and 8 channels), 64-row tiles (32x256 for <= 32 rows)."""
+    if layer.wdtype == WDT_BF16:
+        return layer
+    kc = 16
+    w32 = layer.w[:layer.cin]                          # [cin, k, m_pad]
+    cin_pad = (layer.cin + kc - 1) // kc * kc
+    k, m_pad = w32.shape[1], w32.shape[2]
+    w = w32.new_zeros(cin_pad, k, m_pad)
+    w[:layer.cin] = w32
+    w = w.view(cin_pad // kc, kc // 8, 8, k, m_pad).permute(0, 3, 1, 4, 2).contiguous()
+    tile = TILE_32x256 if layer.m <= 32 else TILE_64x128
+    return PackedConv(w.to(torch.bfloat16), layer.bias, layer.cin, layer.m, layer.k, layer.dil,
+                      layer.pad_left, layer.epi, tile, kc, up_u=layer.up_u, up_pad=layer.up_pad,
+                      out_channels=layer.out_channels, extra=layer.extra, wdtype=WDT_BF16)
 
 
 def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], *, dilation: int = 1,
@@ -162,8 +204,9 @@ def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], *, dilation: i
     tile = _pick_tile(cout, k)
     packed, kc = _finish_pack(rows, k, tile, dilation)
     b = None if bias is None else bias.detach().to(torch.float32).contiguous()
-    return PackedConv(packed, b, cin, cout, k, dilation, padding, epi, tile, kc,
-                      out_channels=outc)
+    layer = PackedConv(packed, b, cin, cout, k, dilation, padding, epi, tile, kc,
+                       out_channels=outc)
+    return to_bf16(layer) if PACK_PRECISION.bf16 else layer
 
 
 def pack_conv_transpose(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
@@ -183,8 +226,9 @@ def pack_conv_transpose(weight: torch.Tensor, bias: Optional[torch.Tensor], stri
     tile = _pick_tile(cout * u, kp)
     packed, kc = _finish_pack(rows, kp, tile)
     b = None if bias is None else bias.detach().to(torch.float32).contiguous()
-    return PackedConv(packed, b, cin, cout * u, kp, 1, kp - 1, EPI_UPSAMPLE, tile, kc,
-                      up_u=u, up_pad=padding, out_channels=cout)
+    layer = PackedConv(packed, b, cin, cout * u, kp, 1, kp - 1, EPI_UPSAMPLE, tile, kc,
+                       up_u=u, up_pad=padding, out_channels=cout)
+    return to_bf16(layer) if PACK_PRECISION.bf16 else layer
 
 
 # ---------------------------------------------------------------------------
@@ -260,6 +304,7 @@ def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Option
     d.out0 = out0
     if out1 is not None:
         d.out1 = out1
+    d.wdtype = layer.wdtype
     return d
 
 
