@@ -87,7 +87,7 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool BF>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool BF, bool V4>
 __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_desc p) {
   constexpr int WM = BM / WAVES_M;
   constexpr int WN = BN / WAVES_N;
@@ -104,11 +104,18 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   const int xw_pad = (xw + 3) & ~3;
   const int wrows = kc * k;
   const int wsz = BF ? wrows * BM / 2 : wrows * BM;  // W stage in float slots
-  const int xsz = kc * xw_pad;  // staged window elements
+  // X window geometry.  Scalar staging (any strides): rows of xw_pad
+  // elements starting at column xstart.  V4 staging (time-contiguous rows,
+  // 16-byte aligned, tin % 4 == 0): 16-byte blocks from the aligned column
+  // xstart - xsh, rows of xrs = 4 * nb elements; the MFMA reads add xsh.
+  const int xsh = V4 ? ((p.pad_left & 3) ? 4 - (p.pad_left & 3) : 0) : 0;  // (-pad_left) mod 4
+  const int nb = (xw + xsh + 3) >> 2;       // V4: 16-byte blocks per window row
+  const int xrs = V4 ? 4 * nb : xw_pad;     // window row length in LDS elements
+  const int xsz = kc * xrs;                 // staged window elements
   // bf16 path: the window sits in LDS as bf16 [t][kc + 4] (channel-contiguous
   // per time step, 8-byte aligned rows) so a B fragment is two ds_read_b64
   const int kcp = kc + 4;
-  const int xslots = BF ? (xw_pad * kcp + 1) / 2 : xsz;  // LDS float slots
+  const int xslots = BF ? (xrs * kcp + 1) / 2 : xsz;  // LDS float slots
   // two stages: [W0][X0][W1][X1]
   float* const stage0 = smem;
   float* const stage1 = smem + wsz + xslots;
@@ -134,20 +141,27 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 
   const float* xb = p.x + (int64_t)b * p.x_bstride;
   const int64_t xts = p.x_tstride;
-  const int xstart = n0 - p.pad_left;
+  const int xstart = n0 - p.pad_left - xsh;  // V4: a multiple of 4
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
   constexpr int MAXX = XTile<BN, BF>::regs;
-  float xreg[MAXX];
-  int xrow[MAXX];  // window row of element tid + 256q (1<<24 when it is padding)
-  int xoff[MAXX];  // its global offset relative to row 0 of the chunk
+  constexpr int NU = V4 ? MAXX / 4 : MAXX;  // staging units per thread (blocks or elements)
+  constexpr int UW = V4 ? 4 : 1;            // elements per unit
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x4v xreg4[V4 ? NU : 1];
+  float xreg[V4 ? 1 : NU];
+  int xrow[NU];  // window row of unit tid + 256q (1<<24 when it is padding)
+  int xoff[NU];  // its global offset relative to row 0 of the chunk
+  const int nunits = V4 ? kc * nb : xsz;
 #pragma unroll
-  for (int q = 0; q < MAXX; ++q) {
-    const int i = tid + q * 256;
-    const int r = i / xw_pad;
-    const int t = i - r * xw_pad;
+  for (int q = 0; q < NU; ++q) {
+    const int u = tid + q * 256;
+    const int per = V4 ? nb : xw_pad;
+    const int r = u / per;
+    const int c = u - r * per;
+    const int t = c * UW;  // first window column of the unit
     const int tt = xstart + t;
-    const bool ok = i < xsz && t < xw && tt >= 0 && tt < p.tin;
+    const bool ok = u < nunits && (V4 || t < xw) && tt >= 0 && tt < p.tin;
     xrow[q] = ok ? r : (1 << 24);
     xoff[q] = ok ? r * p.x_cstride + tt * (int)xts : 0;
   }
@@ -181,10 +195,14 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
     const float* base = xb + (int64_t)c0 * p.x_cstride;
     const int lim = p.cin - c0;  // rows >= lim are channel padding
 #pragma unroll
-    for (int q = 0; q < MAXX; ++q) {
-      if (q * 256 < xsz) {  // workgroup-uniform: no exec-mask branch
+    for (int q = 0; q < NU; ++q) {
+      if (q * 256 < nunits) {  // workgroup-uniform: no exec-mask branch
         const bool ok = xrow[q] < lim;
-        xreg[q] = *(ok ? base + xoff[q] : xb);
+        const float* src = ok ? base + xoff[q] : xb;
+        if constexpr (V4)
+          xreg4[q] = *reinterpret_cast<const f32x4v*>(src);
+        else
+          xreg[q] = *src;
       }
     }
   };
@@ -193,19 +211,39 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
     float* xs = st + wsz;
     const int lim = p.cin - c0;
 #pragma unroll
-    for (int q = 0; q < MAXX; ++q) {
-      if (q * 256 < xsz) {
-        const int i = tid + q * 256;
-        float v = xreg[q];
-        if (act_in) v = v < 0.f ? v * slope : v;
-        v = xrow[q] < lim ? v : 0.f;
-        if (i < xsz) {
-          if constexpr (BF) {
-            const int r = i / xw_pad;
-            const int t = i - r * xw_pad;
-            reinterpret_cast<__bf16*>(xs)[t * kcp + r] = (__bf16)v;
+    for (int q = 0; q < NU; ++q) {
+      if (q * 256 < nunits) {
+        const int u = tid + q * 256;
+        const bool ok = xrow[q] < lim;
+        if (u < nunits) {
+          if constexpr (V4) {
+            f32x4v v = xreg4[q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float t = v[e];
+              if (act_in) t = t < 0.f ? t * slope : t;
+              v[e] = ok ? t : 0.f;
+            }
+            const int r = u / nb;
+            const int c = u - r * nb;
+            if constexpr (BF) {
+              __bf16* xh = reinterpret_cast<__bf16*>(xs);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) xh[(4 * c + e) * kcp + r] = (__bf16)v[e];
+            } else {
+              *reinterpret_cast<f32x4v*>(xs + r * xrs + 4 * c) = v;
+            }
           } else {
-            xs[i] = v;
+            float v = xreg[q];
+            if (act_in) v = v < 0.f ? v * slope : v;
+            v = ok ? v : 0.f;
+            if constexpr (BF) {
+              const int r = u / xw_pad;
+              const int t = u - r * xw_pad;
+              reinterpret_cast<__bf16*>(xs)[t * kcp + r] = (__bf16)v;
+            } else {
+              xs[u] = v;
+            }
           }
         }
       }
@@ -248,7 +286,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 #pragma unroll
           for (int ni = 0; ni < TN; ++ni) {
             const __bf16* xp = reinterpret_cast<const __bf16*>(xs) +
-                               (wn + ni * 32 + l32 + j * dil) * kcp + 16 * g + 8 * lhi;
+                               (wn + ni * 32 + l32 + j * dil + xsh) * kcp + 16 * g + 8 * lhi;
             typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
             const bf16x4 lo = *reinterpret_cast<const bf16x4*>(xp);
             const bf16x4 hi = *reinterpret_cast<const bf16x4*>(xp + 4);
@@ -268,9 +306,9 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
       // the read after the last step runs past the chunk into padded LDS and
       // is never consumed.
       const float* wa = ws + lhi * k * BM + wm + l32;
-      const float* xa = xs + lhi * xw_pad + wn + l32;
+      const float* xa = xs + lhi * xrs + wn + l32 + xsh;
       const int sa = 2 * k * BM;
-      const int sb = 2 * xw_pad;
+      const int sb = 2 * xrs;
       int j = 0, cp = 0;
       const float* pa = wa;
       const float* pb = xa;
@@ -454,39 +492,54 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   }
 }
 
-template <int BM, int BN, int WM_, int WN_, bool BF>
-int launch_tile(const vits_conv1d_desc& d, int batch, hipStream_t s) {
-  const int halo = (d.k - 1) * d.dil;
-  const int xw_pad = (BN + halo + 3) & ~3;
+template <int BM, int BN, int WM_, int WN_, bool BF, bool V4>
+int launch_tile_v(const vits_conv1d_desc& d, int batch, hipStream_t s, size_t xrs) {
   const size_t wsz = BF ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
-  const size_t xsz = (size_t)d.kc * xw_pad;
+  const size_t xsz = (size_t)d.kc * xrs;
   if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) || xsz > (size_t)XTile<BN, BF>::floats)
     return VITS_E_UNSUP;
-  const size_t xslots = BF ? ((size_t)xw_pad * (d.kc + 4) + 1) / 2 : xsz;
   // 32-bit window offsets
   if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
     return VITS_E_UNSUP;
+  const size_t xslots = BF ? (xrs * (d.kc + 4) + 1) / 2 : xsz;
   // + tail pad: the software pipeline reads one k-step past the last chunk
-  const size_t lds = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xw_pad + 64);
+  const size_t lds = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xrs + 64);
   dim3 grid((d.n_out + BN - 1) / BN, (d.m + BM - 1) / BM, batch);
   dim3 block(256);
   switch (d.epi) {
     case VITS_EPI_STORE:
       if (d.split < d.m)
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, BF>), grid, block, lds, s, d);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, BF, V4>), grid, block, lds, s, d);
       else
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, BF>), grid, block, lds, s, d);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, BF, V4>), grid, block, lds, s, d);
       break;
     case VITS_EPI_GATE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, BF>), grid, block, lds, s, d);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, BF, V4>), grid, block, lds, s, d);
       break;
     case VITS_EPI_UPSAMPLE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, BF>), grid, block, lds, s, d);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, BF, V4>), grid, block, lds, s, d);
       break;
     default:
       return VITS_E_UNSUP;
   }
   return vits_launch_status();
+}
+
+// 16-byte X staging when every window row is a 16-byte-aligned run of time
+// steps (the [B][C][T] activations with T % 4 == 0) and the wider window
+// still fits the stage; element-wise staging otherwise
+template <int BM, int BN, int WM_, int WN_, bool BF>
+int launch_tile(const vits_conv1d_desc& d, int batch, hipStream_t s) {
+  const int xw = BN + (d.k - 1) * d.dil;
+  const int xw_pad = (xw + 3) & ~3;
+  const int xsh = (d.pad_left & 3) ? 4 - (d.pad_left & 3) : 0;
+  const int xrs4 = 4 * ((xw + xsh + 3) >> 2);
+  const bool v4 = d.x_tstride == 1 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
+                  (d.tin & 3) == 0 && d.pad_left >= 0 &&
+                  (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
+                  (size_t)d.kc * xrs4 <= (size_t)XTile<BN, BF>::floats;
+  if (v4) return launch_tile_v<BM, BN, WM_, WN_, BF, true>(d, batch, s, xrs4);
+  return launch_tile_v<BM, BN, WM_, WN_, BF, false>(d, batch, s, xw_pad);
 }
 
 int check_desc(const vits_conv1d_desc& d, int batch) {

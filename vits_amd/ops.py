@@ -93,7 +93,8 @@ def _pick_kc(cin: int, k: int, dil: int, tile: int) -> int:
     occupancy (the conv is latency-bound at small K: on MI355X a 64x128 k=3
     conv runs 86 TF/s at kc=10 / 5 WGs per CU but 77 TF/s at kc=14 / 4)."""
     bm, bn = TILE_ROWS[tile], TILE_COLS[tile]
-    xw_pad = (bn + (k - 1) * dil + 3) // 4 * 4
+    # + 4: the 16-byte staging path aligns the window start down to 4 columns
+    xw_pad = (bn + (k - 1) * dil + 3) // 4 * 4 + 4
     lds_fixed = 4 * (2 * k * bm + 2 * xw_pad + 64)
     lds_floats = (LDS_BYTES_PER_CU // TILE_OCCUPANCY[tile] - lds_fixed) // 8  # per stage, W+X
     occ_kc = lds_floats // (k * bm + xw_pad)
