@@ -18,7 +18,9 @@ Extra fields:
                 against the fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
   cpu_baseline  the CPU oracle (oracle/vits_oracle.py, torch fp32 CPU: the
                 reference algorithm restated) on a bounded sample.
-  longform      BASELINE C5 (30 s utterances, B=4, hipGraph replay).
+  longform      BASELINE C5 (30 s utterances, B=4, bf16 model on the bf16-MFMA
+                conv variant, hipGraph replay), with the fp32 time and the
+                bf16-vs-fp32 waveform SNR beside it.
   train         the metric's second half (BASELINE configs 3/4): train utt/s of
                 the train_stft step (vits_amd/train.py: G fwd/bwd, MWSD D,
                 HIP MAS + MR-STFT, fp16 autocast, AdamW/RAdam) at
@@ -35,6 +37,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -121,29 +124,41 @@ def pmc_traffic():
     return c.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
-def longform_leg(model, device, rank, steps=5, warmup=2, B=4, Tx=500, Ty=2500):
-    """BASELINE C5: 30 s utterances (B=4, Tx=500, Ty=2500 -> 480,000 samples
-    each), the whole infer_p2 replayed from one captured hipGraph."""
-    inputs = make_inputs(B, Tx, Ty, device, seed=4321 + rank)
+def _graph_rate(model, inputs, B, Ty, steps, warmup):
     with torch.no_grad():
-        run = model.capture_infer_p2(B, Tx, Ty)
+        run = model.capture_infer_p2(B, inputs[0].shape[2], Ty)
         for _ in range(warmup):
             run(*inputs)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            run(*inputs)
+            out = run(*inputs)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+    return el, out.float().clone()
+
+
+def longform_leg(model, device, rank, steps=5, warmup=2, B=4, Tx=500, Ty=2500):
+    """BASELINE C5: 30 s utterances (B=4, Tx=500, Ty=2500 -> 480,000 samples
+    each), bf16 model (bf16-MFMA convs, fp32 accumulation and activations),
+    the whole infer_p2 replayed from one captured hipGraph.  The fp32 model
+    is timed on the same inputs and its output is the SNR reference."""
+    inputs = make_inputs(B, Tx, Ty, device, seed=4321 + rank)
+    el32, ref = _graph_rate(model, inputs, B, Ty, steps, warmup)
+    m16 = build_model(device).to(torch.bfloat16)  # same deterministic weights, bf16
+    el16, out = _graph_rate(m16, inputs, B, Ty, steps, warmup)
+    noise = float(((out - ref) ** 2).sum())
+    snr = 10.0 * math.log10(float((ref ** 2).sum()) / max(noise, 1e-30))
     samples = steps * B * Ty * HOP
-    del run
+    del m16
     torch.cuda.empty_cache()
-    return {"value": round(samples / el, 1), "unit": "output samples/s",
-            "ms_per_step": round(el / steps * 1e3, 3), "steps": steps, "warmup": warmup,
-            "x_realtime_22k": round(samples / el / 22050.0, 1), "dtype": "fp32",
+    return {"value": round(samples / el16, 1), "unit": "output samples/s",
+            "ms_per_step": round(el16 / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "x_realtime_22k": round(samples / el16 / 22050.0, 1), "dtype": "bf16",
+            "snr_db_vs_fp32": round(snr, 1),
+            "fp32_ms_per_step": round(el32 / steps * 1e3, 3),
             "workload": f"infer_p2 batch={B} Tx={Tx} Ty={Ty} ({Ty * HOP / SR:.0f} s @16 kHz), "
-                        "whole step replayed from one hipGraph",
-            "note": "C5 asks bf16; this line is the fp32 kernels (a bf16 conv path is not built yet)"}
+                        "bf16 model, whole step replayed from one hipGraph"}
 
 
 def train_leg(args, device, rank, world, dist):

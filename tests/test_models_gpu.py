@@ -223,3 +223,18 @@ def test_generator_vs_oracle(base, device):
     ref = V.generator(oracle_sd(base), z, gg, BASE_MODEL)
     assert got.shape == ref.shape == (2, 1, 37 * 192)
     assert snr_db(got, ref) >= SNR_DB and rel_err(got, ref) < REL
+
+
+def test_bf16_model_infer_p2_vs_reference(device):
+    """A bf16 model runs its convs on the bf16-MFMA kernel variant (fp32
+    activations / accumulation).  Tolerance: waveform SNR >= 30 dB against the
+    reference's fp32 golden output (measured ~40 dB; bf16 weights and
+    inputs round at 2^-8)."""
+    m = base_model(device).to(torch.bfloat16)
+    gd = golden("base_infer.npz")
+    wav = m.infer_p2(T(gd["attn"], device), T(gd["m_p"], device), T(gd["s_p"], device),
+                     T(gd["g"], device), T(gd["noise"], device))
+    assert wav.shape == gd["wav"].shape
+    assert snr_db(wav.float(), gd["wav"]) >= 30.0
+    plan = m.dec.__dict__.get("_vits_amd_plan")
+    assert plan is not None and plan.conv_pre.wdtype == 1  # bf16 kernels were used

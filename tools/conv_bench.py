@@ -66,7 +66,7 @@ for name, cin, cout, k, d, T, gate, up in shapes:
     if tiles:
         t0, kc0 = desc.tile, desc.kc
         for t in tiles:
-            if layer.m_pad % 128 == 0 and (t != 0 or layer.tile == 0):
+            if layer.m_pad % 128 == 0:
                 best = None
                 for mlt in kcms:
                     kc = kc0 * mlt
