@@ -58,19 +58,30 @@ def weight_norm_effective(module: torch.nn.Module, name: str = "weight") -> torc
 
 
 def _pick_tile(m: int, k: int) -> int:
-    """Workgroup tile by GEMM rows and taps, from the per-shape sweep of
-    tools/conv_bench.py on MI355X (B=16, Ty=500 decoder/flow shapes):
-    32 rows -> 32x256; k <= 4 (k=3 resblock convs, 2-tap polyphase ups,
-    1x1) -> 64x128; k = 5..9 and 64/128-row k=11 -> 64x256; k=11 with
-    more rows -> 128x128.  Grids too small to fill the chip twice fall back
+    """fp32 workgroup tile by GEMM rows and taps, from the per-shape sweep of
+    tools/conv_bench.py on MI355X (B=16, Ty=500 decoder/flow shapes, 16-byte
+    X staging): 32 rows -> 32x256; the 2-tap polyphase ups and 1x1 convs ->
+    64x128; everything else -> 64x256 (k=3: +3..5 %, k=7: +6 %, k=11: +5 %
+    over 128x128 / 64x128).  Grids too small to fill the chip twice fall back
     to 64x128 at launch (conv1d.hip)."""
     if m <= 32:
         return TILE_32x256
-    if k <= 4:
+    if k <= 2:
         return TILE_64x128
-    if k <= 9 or m <= 128:
+    return TILE_64x256
+
+
+def _pick_tile_bf16(m: int, k: int) -> int:
+    """bf16-MFMA tile (same sweep, BF=1): short kernels on >= 128 rows are
+    fastest as 128x128 (k=3: 430 vs 340 TF/s), long ones as 64x256
+    (k=11: 730 vs 555), 64-row k<=7 as 64x128, 32 rows as 32x256."""
+    if m <= 32:
+        return TILE_32x256
+    if k <= 3:
+        return TILE_128x128 if m >= 128 else TILE_64x128
+    if m >= 128 or k >= 9:
         return TILE_64x256
-    return TILE_128x128
+    return TILE_64x128
 
 
 TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, TILE_64x128: 128}
@@ -171,7 +182,7 @@ def pack_bf16(enabled: bool = True):
 def to_bf16(layer: PackedConv) -> PackedConv:
     """Re-pack an fp32 layer for the bf16-MFMA kernel variant: K-chunks of 16
     channels, W as [cin_pad/16][k][2][m_pad][8] bf16 (one 16-byte A fragment
-    per row and 8 channels), 64-row tiles (32x256 for <= 32 rows)."""
+    per row and 8 channels), tile by _pick_tile_bf16."""
     if layer.wdtype == WDT_BF16:
         return layer
     kc = 16
@@ -181,7 +192,7 @@ def to_bf16(layer: PackedConv) -> PackedConv:
     w = w32.new_zeros(cin_pad, k, m_pad)
     w[:layer.cin] = w32
     w = w.view(cin_pad // kc, kc // 8, 8, k, m_pad).permute(0, 3, 1, 4, 2).contiguous()
-    tile = TILE_32x256 if layer.m <= 32 else TILE_64x128
+    tile = _pick_tile_bf16(layer.m, layer.k)
     return PackedConv(w.to(torch.bfloat16), layer.bias, layer.cin, layer.m, layer.k, layer.dil,
                       layer.pad_left, layer.epi, tile, kc, up_u=layer.up_u, up_pad=layer.up_pad,
                       out_channels=layer.out_channels, extra=layer.extra, wdtype=WDT_BF16)
