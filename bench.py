@@ -21,6 +21,8 @@ Extra fields:
   longform      BASELINE C5 (30 s utterances, B=4, bf16 model on the bf16-MFMA
                 conv variant, hipGraph replay), with the fp32 time and the
                 bf16-vs-fp32 waveform SNR beside it.
+  kernels       the training-side HIP kernels at C3 shapes against their
+                rooflines (MAS, neg_cent, MR-STFT magnitudes).
   train         the metric's second half (BASELINE configs 3/4): train utt/s of
                 the train_stft step (vits_amd/train.py: G fwd/bwd, MWSD D,
                 HIP MAS + MR-STFT, fp16 autocast, AdamW/RAdam) at
@@ -161,6 +163,67 @@ def longform_leg(model, device, rank, steps=5, warmup=2, B=4, Tx=500, Ty=2500):
                         "bf16 model, whole step replayed from one hipGraph"}
 
 
+def _event_ms(fn, reps=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def kernels_leg(device):
+    """The training-side HIP kernels at BASELINE C3 shapes (B=64, t_t=500
+    frames, t_s=100 tokens, 9216-sample segments), each against its roofline
+    (SURVEY §8(d)): MAS (latency-bound DP; HBM fraction reported), MR-STFT
+    magnitudes (HBM), neg_cent (fp32 MFMA)."""
+    from vits_amd import ops
+    from vits_amd.stft_loss import MultiResolutionSTFTLoss
+
+    g = torch.Generator(device="cpu").manual_seed(7)
+    B, Tt, Ts, C, L = 64, 500, 100, 192, 9216
+    nc = torch.randn(B, Tt, Ts, generator=g).to(device)
+    tt = torch.full((B,), Tt, dtype=torch.int32, device=device)
+    ts = torch.full((B,), Ts, dtype=torch.int32, device=device)
+    mas_ms = _event_ms(lambda: ops.maximum_path_lengths(nc, tt, ts))
+    mas_bytes = B * Tt * Ts * 8
+    z = torch.randn(B, C, Tt, generator=g).to(device)
+    m = torch.randn(B, C, Ts, generator=g).to(device)
+    lg = (torch.randn(B, C, Ts, generator=g) * 0.5).to(device)
+    nc_ms = _event_ms(lambda: ops.neg_cent(z, m, lg))
+    nc_flops = 2 * 2 * C * Tt * Ts * B
+    loss = MultiResolutionSTFTLoss().to(device)
+    y = (torch.randn(B, L, generator=g) * 0.1).to(device)
+    yh = (torch.randn(B, L, generator=g) * 0.1).to(device).requires_grad_(True)
+    fwd_ms = _event_ms(lambda: [f.mag(y) for f in loss.stft_losses])
+    mags = sum((f.fft_size // 2 + 1) * (L // f.hop_size + 1) for f in loss.stft_losses)
+    fwd_bytes = B * (len(loss.stft_losses) * L * 4 + mags * 4)
+
+    def fb():
+        sc, mg, _, _ = loss(yh, y)
+        (sc + mg).backward()
+
+    fb_ms = _event_ms(fb, reps=10)
+    peak = 8000.0
+    return {
+        "mas": {"ms": round(mas_ms, 4), "us_per_utt": round(mas_ms * 1e3 / B, 2),
+                "shape": f"B={B} t_t={Tt} t_s={Ts}", "GBps": round(mas_bytes / mas_ms / 1e6, 1),
+                "frac_hbm": round(mas_bytes / mas_ms / 1e6 / peak, 4),
+                "bound": "latency (t_t sequential DP rows per utterance)"},
+        "neg_cent": {"ms": round(nc_ms, 4), "TFLOPs": round(nc_flops / nc_ms / 1e9, 2),
+                     "frac_fp32_mfma": round(nc_flops / nc_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "shape": f"B={B} C={C} t_t={Tt} t_s={Ts}"},
+        "mrstft_mag_fwd": {"ms": round(fwd_ms, 4), "GBps": round(fwd_bytes / fwd_ms / 1e6, 1),
+                           "frac_hbm": round(fwd_bytes / fwd_ms / 1e6 / peak, 4),
+                           "shape": f"B={B} L={L} x 5 resolutions (one signal)"},
+        "mrstft_loss_fwd_bwd_ms": round(fb_ms, 4),
+    }
+
+
 def train_leg(args, device, rank, world, dist):
     """Timed train_stft steps (BASELINE C3/C4) on synthetic base.json batches."""
     from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
@@ -220,6 +283,7 @@ def main():
     ap.add_argument("--train-warmup", type=int, default=2)
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--no-longform", action="store_true")
+    ap.add_argument("--no-kernels", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -285,6 +349,7 @@ def main():
                     "conv_ms_per_step": round(s["total_ms"] / args.steps, 3)}
 
     longform = None if args.no_longform else longform_leg(model, device, rank)
+    kern = None if args.no_kernels else kernels_leg(device)
 
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if dist:
@@ -312,6 +377,7 @@ def main():
             "x_realtime_22k": round(value / world / 22050.0, 1),
             "roofline": roof,
             "longform": longform,
+            "kernels": kern,
             "train": train,
         }
         if not args.no_cpu_baseline and world == 1:

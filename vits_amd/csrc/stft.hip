@@ -25,14 +25,28 @@ __device__ __forceinline__ int reflect_idx(int i, int L) {
   return i;
 }
 
+// Twiddle table tw[m] = (cos, sin)(2 pi m / n), m < n/2, built once per
+// workgroup (n/2 sincospif instead of one per butterfly and stage).
+__device__ void fill_twiddles(float2* tw, int n) {
+  for (int m = threadIdx.x; m < (n >> 1); m += blockDim.x) {
+    float sn, cs;
+    sincospif(2.0f * (float)m / (float)n, &sn, &cs);
+    tw[m] = make_float2(cs, sn);
+  }
+}
+
 // Stockham radix-2 over FPB independent transforms of size n laid out
 // back to back in `a`; result ends in the returned buffer.  sign = -1
-// forward (e^{-i}), +1 inverse (unnormalised).
-__device__ float2* fft_lds(float2* a, float2* b, int n, int log2n, int fpb, float sign) {
+// forward (e^{-i}), +1 inverse (unnormalised).  Stage s twiddle of butterfly
+// kk is e^{sign i pi kk / 2^s} = tw[kk << (log2n - 1 - s)] (sin negated for
+// the forward transform).
+__device__ float2* fft_lds(float2* a, float2* b, const float2* tw, int n, int log2n, int fpb,
+                           float sign) {
   const int half = n >> 1;
   const int total = fpb * half;
   for (int s = 0; s < log2n; ++s) {
     const int ns = 1 << s;
+    const int tsh = log2n - 1 - s;
     for (int i = threadIdx.x; i < total; i += blockDim.x) {
       const int f = i / half;
       const int j = i - f * half;
@@ -41,8 +55,9 @@ __device__ float2* fft_lds(float2* a, float2* b, int n, int log2n, int fpb, floa
       const int kk = j & (ns - 1);
       const float2 v0 = src[j];
       float2 v1 = src[j + half];
-      float sn, cs;
-      sincospif(sign * (float)kk / (float)ns, &sn, &cs);
+      const float2 w = tw[kk << tsh];
+      const float cs = w.x;
+      const float sn = sign * w.y;
       const float tr = v1.x * cs - v1.y * sn;
       const float ti = v1.x * sn + v1.y * cs;
       const int d = ((j - kk) << 1) + kk;
@@ -67,6 +82,8 @@ __global__ __launch_bounds__(256) void stft_fwd_kernel(const float* __restrict__
   extern __shared__ float2 sfft[];
   float2* a = sfft;
   float2* bbuf = sfft + fpb * n;
+  float2* tw = bbuf + fpb * n;
+  fill_twiddles(tw, n);
   const int b = blockIdx.y;
   const int f0 = blockIdx.x * fpb;
   const int woff = (n - win) / 2;
@@ -84,7 +101,7 @@ __global__ __launch_bounds__(256) void stft_fwd_kernel(const float* __restrict__
     a[i] = make_float2(v, 0.f);
   }
   __syncthreads();
-  const float2* out = fft_lds(a, bbuf, n, log2n, fpb, -1.f);
+  const float2* out = fft_lds(a, bbuf, tw, n, log2n, fpb, -1.f);
   const int nb = n / 2 + 1;
   for (int i = threadIdx.x; i < fpb * nb; i += blockDim.x) {
     const int k = i / fpb;
@@ -106,6 +123,8 @@ __global__ __launch_bounds__(256) void stft_bwd_frames_kernel(
   extern __shared__ float2 sfft[];
   float2* a = sfft;
   float2* bbuf = sfft + fpb * n;
+  float2* tw = bbuf + fpb * n;
+  fill_twiddles(tw, n);
   const int b = blockIdx.y;
   const int f0 = blockIdx.x * fpb;
   const int nb = n / 2 + 1;
@@ -123,7 +142,7 @@ __global__ __launch_bounds__(256) void stft_bwd_frames_kernel(
     a[f * n + k] = g;
   }
   __syncthreads();
-  const float2* out = fft_lds(a, bbuf, n, log2n, fpb, +1.f);
+  const float2* out = fft_lds(a, bbuf, tw, n, log2n, fpb, +1.f);
   for (int i = threadIdx.x; i < fpb * n; i += blockDim.x) {
     const int f = i / n;
     const int t = i - f * n;
@@ -194,7 +213,7 @@ extern "C" int vits_stft_mag_forward(const float* x, int batch, int length, cons
   const int frames = (length + 2 * pad - n_fft) / hop + 1;
   VITS_CHECK_SHAPE(frames > 0);
   const int fpb = n_fft >= 1024 ? 1 : 1024 / n_fft;
-  const size_t lds = sizeof(float2) * 2 * fpb * n_fft;
+  const size_t lds = sizeof(float2) * (2 * fpb * n_fft + n_fft / 2);
   dim3 grid((frames + fpb - 1) / fpb, batch);
   hipLaunchKernelGGL(stft_fwd_kernel, grid, dim3(256), lds, as_stream(stream), x, length, window,
                      n_fft, log2n, hop, win, pad, frames, fpb, eps, mag, re, im);
@@ -213,7 +232,7 @@ extern "C" int vits_stft_mag_backward(const float* grad_mag, const float* mag, c
   VITS_CHECK_SHAPE(frames > 0);
   if (workspace_floats < vits_stft_workspace(batch, length, n_fft, hop, pad)) return VITS_E_ARG;
   const int fpb = n_fft >= 1024 ? 1 : 1024 / n_fft;
-  const size_t lds = sizeof(float2) * 2 * fpb * n_fft;
+  const size_t lds = sizeof(float2) * (2 * fpb * n_fft + n_fft / 2);
   hipStream_t s = as_stream(stream);
   dim3 grid((frames + fpb - 1) / fpb, batch);
   hipLaunchKernelGGL(stft_bwd_frames_kernel, grid, dim3(256), lds, s, grad_mag, mag, re, im,
