@@ -176,6 +176,33 @@ def _event_ms(fn, reps=20, warmup=3):
     return s.elapsed_time(e) / reps
 
 
+def latency_leg(model, device, reps=10):
+    """Serving latency (EmoVITS / VITSWrap call pattern, one utterance):
+    infer_p1 (text encoder + duration predictor) + infer_p2 (flow + decoder)
+    at Tx=100, Ty=500 (96,000 samples = 6 s at 16 kHz), B=1, fp32."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(1, 100, 256, generator=g).to(device)
+    emo = torch.randn(1, 1024, generator=g).to(device)
+    sid = torch.tensor([1], device=device)
+    attn, _, _, _, noise = make_inputs(1, 100, 500, device)
+
+    def once():
+        m_p, s_p, logw, gg = model.infer_p1(x, emo, sid)
+        return model.infer_p2(attn, m_p, s_p, gg, noise)
+
+    with torch.no_grad():
+        for _ in range(3):
+            once()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            once()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"ms": round(ms, 3), "audio_s": 6.0, "rtf_16k": round(ms / 6000.0, 6),
+            "workload": "infer_p1 + infer_p2, B=1, Tx=100, Ty=500, fp32, eager"}
+
+
 def kernels_leg(device):
     """The training-side HIP kernels at BASELINE C3 shapes (B=64, t_t=500
     frames, t_s=100 tokens, 9216-sample segments), each against its roofline
@@ -350,6 +377,7 @@ def main():
 
     longform = None if args.no_longform else longform_leg(model, device, rank)
     kern = None if args.no_kernels else kernels_leg(device)
+    latency = None if args.no_kernels else latency_leg(model, device)
 
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if dist:
@@ -378,6 +406,7 @@ def main():
             "roofline": roof,
             "longform": longform,
             "kernels": kern,
+            "latency_b1": latency,
             "train": train,
         }
         if not args.no_cpu_baseline and world == 1:
