@@ -118,14 +118,16 @@ typedef struct vits_conv1d_desc {
   vits_conv_out out0;
   vits_conv_out out1;
   /* weight / MFMA type: VITS_WDT_F32 (w as above, exact-f32 MFMA) or      */
-  /* VITS_WDT_BF16 (w = bf16 [cin_pad/kc][k][kc/8][m_pad][8], kc % 16 == 0, */
-  /* activations still fp32 in HBM, rounded to bf16 when staged, fp32      */
-  /* accumulation: v_mfma_f32_32x32x16_bf16)                                */
+  /* VITS_WDT_BF16 / VITS_WDT_F16 (w = 16-bit [cin_pad/kc][k][kc/8][m_pad]  */
+  /* [8], kc % 16 == 0; activations stay fp32 in HBM and are rounded to the */
+  /* 16-bit type when staged; fp32 accumulation:                           */
+  /* v_mfma_f32_32x32x16_bf16 / _f16)                                       */
   int32_t wdtype;
 } vits_conv1d_desc;
 
 #define VITS_WDT_F32 0
 #define VITS_WDT_BF16 1
+#define VITS_WDT_F16 2
 
 int vits_conv1d_forward(const vits_conv1d_desc* d, int batch, void* stream);
 

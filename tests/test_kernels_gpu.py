@@ -290,23 +290,27 @@ def test_neg_cent(device, B, C, Tt, Ts):
 # accumulation order only), and with the fp32 conv loosely (bf16 rounding).
 # --------------------------------------------------------------------------
 
-def _bf(t):
-    return t.to(torch.bfloat16).double()
+def _bf(t, dt=torch.bfloat16):
+    return t.to(dt).double()
 
 
+_LOWP = {torch.bfloat16: 1, torch.float16: 2}
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,cin,cout,k,dil,T,gate", [
     (2, 256, 256, 3, 1, 300, True), (1, 128, 128, 11, 5, 777, True), (2, 64, 128, 7, 1, 500, False),
     (3, 16, 32, 11, 1, 1000, False), (2, 32, 32, 3, 5, 2000, True), (1, 192, 512, 7, 1, 101, False),
     (2, 513, 256, 1, 1, 64, False), (1, 24, 40, 5, 2, 90, False),
 ])
-def test_conv1d_bf16(device, B, cin, cout, k, dil, T, gate):
+def test_conv1d_bf16(device, B, cin, cout, k, dil, T, gate, dt):
     g = torch.Generator().manual_seed(B * 100 + cin + k)
     x = torch.randn(B, cin, T, generator=g)
     w = torch.randn(cout, cin, k, generator=g) / (cin * k) ** 0.5
     b = torch.randn(cout, generator=g) * 0.1
     pad = (k * dil - dil) // 2
     xa = F.leaky_relu(x, 0.1)
-    yq = F.conv1d(_bf(xa), _bf(w), b.double(), padding=pad, dilation=dil)
+    yq = F.conv1d(_bf(xa, dt), _bf(w, dt), b.double(), padding=pad, dilation=dil)
     cond = torch.randn(B, cout, generator=g) if gate else None
     res = None if gate else torch.randn(B, cout, T, generator=g)
     if gate:
@@ -315,24 +319,26 @@ def test_conv1d_bf16(device, B, cin, cout, k, dil, T, gate):
         ref = torch.tanh(ya + sa.unsqueeze(-1)) * torch.sigmoid(yb + sb.unsqueeze(-1))
     else:
         ref = yq + res.double()
-    with ops.pack_bf16():
+    with ops.pack_lowp(_LOWP[dt]):
         layer = ops.pack_conv(w.to(device), b.to(device), dilation=dil, gate=gate)
-    assert layer.wdtype == 1
+    assert layer.wdtype == _LOWP[dt] and layer.w.dtype == dt
     out = ops.conv1d(x.to(device), layer, in_slope=0.1,
                      cond=None if cond is None else cond.to(device),
                      residual=None if res is None else res.to(device))
     _close(out, ref, tol=2e-5, what="bf16 conv vs bf16-rounded fp64")
 
 
-def test_conv_transpose_bf16(device):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_conv_transpose_bf16(device, dt):
     g = torch.Generator().manual_seed(5)
     B, cin, cout, K, u, T = 2, 256, 128, 12, 6, 57
     x = torch.randn(B, cin, T, generator=g)
     w = torch.randn(cin, cout, K, generator=g) / (cin * 2) ** 0.5
     b = torch.randn(cout, generator=g) * 0.1
     pad = (K - u) // 2
-    ref = F.conv_transpose1d(_bf(F.leaky_relu(x, 0.1)), _bf(w), b.double(), stride=u, padding=pad)
-    with ops.pack_bf16():
+    ref = F.conv_transpose1d(_bf(F.leaky_relu(x, 0.1), dt), _bf(w, dt), b.double(), stride=u,
+                             padding=pad)
+    with ops.pack_lowp(_LOWP[dt]):
         layer = ops.pack_conv_transpose(w.to(device), b.to(device), u, pad)
     out = ops.conv1d(x.to(device), layer, in_slope=0.1)
     _close(out, ref, tol=2e-5, what="bf16 convT")

@@ -1,0 +1,579 @@
+// conv1d_impl.h — the templated MFMA conv kernel and its launchers, shared
+// by the per-operand-type translation units conv1d_{f32,bf16,f16}.hip (one
+// instantiation set each, compiled in parallel).  See conv1d.hip for the
+// design notes.
+#pragma once
+#include "common.h"
+
+namespace vits_conv {
+
+
+// internal epilogue variant: STORE with a second output descriptor (row split)
+constexpr int EPI_STORE2 = 100;
+
+struct OutDesc {
+  float* y;
+  int64_t y_bstride;
+  int y_cstride;
+  int act;
+  const float* res;
+  int64_t res_bstride;
+  int res_cstride;
+  float res_scale;
+  int accumulate;
+  float post_div;
+};
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == VITS_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == VITS_ACT_TANH) return tanhf(v);
+  if (act == VITS_ACT_EXP) return expf(v);
+  return v;
+}
+
+__device__ __forceinline__ void store_std(const OutDesc& o, int b, int ch, int t, float v,
+                                          bool masked) {
+  v = apply_act(v, o.act);
+  if (o.res) v = o.res[(int64_t)b * o.res_bstride + (int64_t)ch * o.res_cstride + t] + o.res_scale * v;
+  float* dst = o.y + (int64_t)b * o.y_bstride + (int64_t)ch * o.y_cstride + t;
+  if (o.accumulate) v = *dst + v;
+  if (o.post_div != 1.0f) v = v / o.post_div;
+  if (masked) v = 0.f;
+  *dst = v;
+}
+
+// Register budget of the global->LDS prefetch (per thread): the host packs
+// layers so that kc*k*BM <= VITS_W_TILE and kc*xw_pad <= VITS_X_TILE floats.
+// W chunks go global->LDS by LDS-DMA (no registers); X chunks are staged
+// through registers (zero padding + leaky-relu prologue on the way).
+constexpr int VITS_W_TILE = 4096;
+// X staging: element i of the chunk's [kc][xw_pad] window (LDS float i) is
+// owned by thread i % 256; its (row, column) -> global offset mapping does
+// not depend on the chunk, so it is computed once per workgroup.  The host
+// keeps kc * xw_pad <= floats.
+template <int BN, bool BF = false>
+struct XTile {
+  // bf16-MFMA chunks carry >= 16 channels: a wider window budget
+  static constexpr int floats = BF ? (BN <= 128 ? 3072 : 5120) : (BN <= 128 ? 2048 : 4096);
+  static constexpr int regs = floats / 256;
+};
+// bf16 W stage budget in float slots (2 bf16 each): k=11, kc=16, BM=64 fits
+constexpr int VITS_W_TILE_BF = 6144;
+// low-precision element type of weight type WT (VITS_WDT_BF16 / VITS_WDT_F16)
+template <int WT>
+struct LowP {
+  typedef __bf16 T;
+};
+template <>
+struct LowP<VITS_WDT_F16> {
+  typedef _Float16 T;
+};
+typedef __attribute__((address_space(3))) void* lds_void_t;
+
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float fast_tanh(float x) {
+  // tanh(x) = 2 sigmoid(2x) - 1 ; |err| ~ 1e-7 absolute
+  return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4>
+__global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_desc p) {
+  constexpr bool BF = WT != VITS_WDT_F32;  // 16-bit operands (bf16 or fp16)
+  typedef typename LowP<WT>::T lp_t;
+  typedef lp_t lpx8 __attribute__((ext_vector_type(8)));
+  typedef lp_t lpx4 __attribute__((ext_vector_type(4)));
+  constexpr int WM = BM / WAVES_M;
+  constexpr int WN = BN / WAVES_N;
+  constexpr int TM = WM / 32;
+  constexpr int TN = WN / 32;
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
+  static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+
+  extern __shared__ float smem[];
+  const int kc = p.kc;
+  const int k = p.k;
+  const int dil = p.dil;
+  const int xw = BN + (k - 1) * dil;
+  const int xw_pad = (xw + 3) & ~3;
+  const int wrows = kc * k;
+  const int wsz = BF ? wrows * BM / 2 : wrows * BM;  // W stage in float slots
+  // X window geometry.  Scalar staging (any strides): rows of xw_pad
+  // elements starting at column xstart.  V4 staging (time-contiguous rows,
+  // 16-byte aligned, tin % 4 == 0): 16-byte blocks from the aligned column
+  // xstart - xsh, rows of xrs = 4 * nb elements; the MFMA reads add xsh.
+  const int xsh = V4 ? ((p.pad_left & 3) ? 4 - (p.pad_left & 3) : 0) : 0;  // (-pad_left) mod 4
+  const int nb = (xw + xsh + 3) >> 2;       // V4: 16-byte blocks per window row
+  const int xrs = V4 ? 4 * nb : xw_pad;     // window row length in LDS elements
+  const int xsz = kc * xrs;                 // staged window elements
+  // bf16 path: the window sits in LDS as bf16 [t][kc + 4] (channel-contiguous
+  // per time step, 8-byte aligned rows) so a B fragment is two ds_read_b64
+  const int kcp = kc + 4;
+  const int xslots = BF ? (xrs * kcp + 1) / 2 : xsz;  // LDS float slots
+  // two stages: [W0][X0][W1][X1]
+  float* const stage0 = smem;
+  float* const stage1 = smem + wsz + xslots;
+
+  const int b = blockIdx.z;
+  const int n0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * BM;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = (wid / WAVES_N) * WM;
+  const int wn = (wid % WAVES_N) * WN;
+  const int l32 = lane & 31;
+  const int lhi = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const float* xb = p.x + (int64_t)b * p.x_bstride;
+  const int64_t xts = p.x_tstride;
+  const int xstart = n0 - p.pad_left - xsh;  // V4: a multiple of 4
+  const float slope = p.in_slope;
+  const bool act_in = slope != 1.0f;
+  constexpr int MAXX = XTile<BN, BF>::regs;
+  constexpr int NU = V4 ? MAXX / 4 : MAXX;  // staging units per thread (blocks or elements)
+  constexpr int UW = V4 ? 4 : 1;            // elements per unit
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x4v xreg4[V4 ? NU : 1];
+  float xreg[V4 ? 1 : NU];
+  int xrow[NU];  // window row of unit tid + 256q (1<<24 when it is padding)
+  int xoff[NU];  // its global offset relative to row 0 of the chunk
+  const int nunits = V4 ? kc * nb : xsz;
+#pragma unroll
+  for (int q = 0; q < NU; ++q) {
+    const int u = tid + q * 256;
+    const int per = V4 ? nb : xw_pad;
+    const int r = u / per;
+    const int c = u - r * per;
+    const int t = c * UW;  // first window column of the unit
+    const int tt = xstart + t;
+    const bool ok = u < nunits && (V4 || t < xw) && tt >= 0 && tt < p.tin;
+    xrow[q] = ok ? r : (1 << 24);
+    xoff[q] = ok ? r * p.x_cstride + tt * (int)xts : 0;
+  }
+
+  // ---- W chunk: LDS-DMA, one 1 KiB piece (256 floats) per wave instruction;
+  // lane l of piece q lands at LDS float q*256 + 4l (lane-linear image)
+  auto wdma = [&](int c0, float* st) {
+    // the chunk's W image is R rows of L float slots, HBM row stride S:
+    //   f32:  [kc*k][BM] rows of W[c][j][m0..m0+BM)
+    //   bf16: [k*kc/8][BM*8 bf16] rows of W[chunk][j][c8][m0..m0+BM][8]
+    const int L = BF ? BM * 4 : BM;
+    const float* wsrc = BF ? p.w + ((int64_t)(c0 / kc) * (k * (kc / 8)) * p.m_pad + m0) * 4
+                           : p.w + (int64_t)c0 * k * p.m_pad + m0;
+    const int64_t S = BF ? (int64_t)p.m_pad * 4 : p.m_pad;
+    const int pieces = (wsz + 255) >> 8;
+    for (int q = wid; q < pieces; q += 4) {
+      const int e = q * 256 + lane * 4;
+      if (e < wsz) {
+        const int r = e / L;
+        const int col = e - r * L;
+        __builtin_amdgcn_global_load_lds(wsrc + (int64_t)r * S + col,
+                                         (lds_void_t)(st + q * 256), 16, 0, 0);
+      }
+    }
+  };
+  // ---- X chunk: global -> registers, raw.  Every lane issues its loads
+  // unconditionally (padding lanes read the batch's first element) so the
+  // compiler cannot tie a wait to each load: all MAXX loads stay in flight
+  // under the chunk's MFMAs and are consumed in lstore.
+  auto gload = [&](int c0) {
+    const float* base = xb + (int64_t)c0 * p.x_cstride;
+    const int lim = p.cin - c0;  // rows >= lim are channel padding
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      if (q * 256 < nunits) {  // workgroup-uniform: no exec-mask branch
+        const bool ok = xrow[q] < lim;
+        const float* src = ok ? base + xoff[q] : xb;
+        if constexpr (V4)
+          xreg4[q] = *reinterpret_cast<const f32x4v*>(src);
+        else
+          xreg[q] = *src;
+      }
+    }
+  };
+  // ---- registers -> LDS stage (zero padding + leaky-relu prologue) -----------
+  auto lstore = [&](float* st, int c0) {
+    float* xs = st + wsz;
+    const int lim = p.cin - c0;
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      if (q * 256 < nunits) {
+        const int u = tid + q * 256;
+        const bool ok = xrow[q] < lim;
+        if (u < nunits) {
+          if constexpr (V4) {
+            f32x4v v = xreg4[q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float t = v[e];
+              if (act_in) t = t < 0.f ? t * slope : t;
+              v[e] = ok ? t : 0.f;
+            }
+            const int r = u / nb;
+            const int c = u - r * nb;
+            if constexpr (BF) {
+              lp_t* xh = reinterpret_cast<lp_t*>(xs);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) xh[(4 * c + e) * kcp + r] = (lp_t)v[e];
+            } else {
+              *reinterpret_cast<f32x4v*>(xs + r * xrs + 4 * c) = v;
+            }
+          } else {
+            float v = xreg[q];
+            if (act_in) v = v < 0.f ? v * slope : v;
+            v = ok ? v : 0.f;
+            if constexpr (BF) {
+              const int r = u / xw_pad;
+              const int t = u - r * xw_pad;
+              reinterpret_cast<lp_t*>(xs)[t * kcp + r] = (lp_t)v;
+            } else {
+              xs[u] = v;
+            }
+          }
+        }
+      }
+    }
+  };
+
+  const int nchunks = p.cin_pad / kc;
+  const int half = kc >> 1;
+  const int steps = k * half;  // MFMA k-steps per chunk
+
+  wdma(0, stage0);
+  gload(0);
+  lstore(stage0, 0);
+  __syncthreads();
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    float* cur = (ch & 1) ? stage1 : stage0;
+    float* nxt = (ch & 1) ? stage0 : stage1;
+    const bool more = ch + 1 < nchunks;
+    if (more) {  // both in flight under the MFMAs below
+      wdma((ch + 1) * kc, nxt);
+      gload((ch + 1) * kc);
+    }
+
+    const float* ws = cur;
+    const float* xs = cur + wsz;
+    if constexpr (BF) {
+      // k-step = (tap j, 16 channels): A = one 16-byte bf16x8 read per
+      // 32-row fragment (W image [j][c8][row][8]); B = 8 channel rows of the
+      // fp32 X window at column n + j*dil, rounded to bf16 in registers
+      const char* wbytes = reinterpret_cast<const char*>(ws);
+      const int c8n = kc >> 3;
+      for (int j = 0; j < k; ++j) {
+        for (int g = 0; g < (kc >> 4); ++g) {
+          lpx8 a[TM], bb[TN];
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi)
+            a[mi] = *reinterpret_cast<const lpx8*>(
+                wbytes + ((int64_t)((j * c8n + 2 * g + lhi) * BM + wm + mi * 32 + l32) << 4));
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) {
+            const lp_t* xp = reinterpret_cast<const lp_t*>(xs) +
+                               (wn + ni * 32 + l32 + j * dil + xsh) * kcp + 16 * g + 8 * lhi;
+            const lpx4 lo = *reinterpret_cast<const lpx4*>(xp);
+            const lpx4 hi = *reinterpret_cast<const lpx4*>(xp + 4);
+            bb[ni] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+              if constexpr (WT == VITS_WDT_F16)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
+              else
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
+        }
+      }
+    } else {
+      // k-step s = (tap j, channel pair cp), cp fastest: A rows (2cp + lhi)*k + j
+      // of W, B row 2cp + lhi of X shifted by j*dil.  Two register sets ping-
+      // pong so the LDS reads of step s+1 are in flight under the MFMAs of s;
+      // the read after the last step runs past the chunk into padded LDS and
+      // is never consumed.
+      const float* wa = ws + lhi * k * BM + wm + l32;
+      const float* xa = xs + lhi * xrs + wn + l32 + xsh;
+      const int sa = 2 * k * BM;
+      const int sb = 2 * xrs;
+      int j = 0, cp = 0;
+      const float* pa = wa;
+      const float* pb = xa;
+      auto advance = [&]() {
+        ++cp;
+        pa += sa;
+        pb += sb;
+        if (cp == half) {
+          cp = 0;
+          ++j;
+          pa = wa + j * BM;
+          pb = xa + j * dil;
+        }
+      };
+      float a0[TM], b0[TN], a1[TM], b1[TN];
+  #pragma unroll
+      for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
+  #pragma unroll
+      for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
+      advance();
+      int s = 0;
+      for (; s + 2 <= steps; s += 2) {
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi) a1[mi] = pa[mi * 32];
+  #pragma unroll
+        for (int ni = 0; ni < TN; ++ni) b1[ni] = pb[ni * 32];
+        advance();
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+  #pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
+  #pragma unroll
+        for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
+        advance();
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+  #pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[mi], b1[ni], acc[mi][ni], 0, 0, 0);
+      }
+      if (s < steps) {
+  #pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+  #pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+      }
+    }
+    if (more) lstore(nxt, (ch + 1) * kc);
+    __syncthreads();
+  }
+
+  // ---- epilogue -----------------------------------------------------------
+  const int len_b = p.lengths ? p.lengths[b] : 0x7fffffff;
+  const float* cond = p.cond ? p.cond + (int64_t)b * p.cond_bstride : nullptr;
+  OutDesc o0{p.out0.y, p.out0.y_bstride, p.out0.y_cstride, p.out0.act, p.out0.res,
+             p.out0.res_bstride, p.out0.res_cstride, p.out0.res_scale, p.out0.accumulate,
+             p.out0.post_div};
+  // per-row additive constant (bias + per-utterance cond) of this tile's BM
+  // rows, fetched once by BM threads in parallel into LDS (the stages are
+  // free after the last barrier of the K loop)
+  float* const erow = smem;
+  if (tid < BM) {
+    const int row = m0 + tid;
+    float e = 0.f;
+    if (row < p.m) {
+      int idx = row;
+      if (EPI == VITS_EPI_GATE) idx = (row & 1) ? (p.m >> 1) + (row >> 1) : (row >> 1);
+      if (EPI == VITS_EPI_UPSAMPLE) idx = row / p.up_u;
+      if (p.bias) e = p.bias[idx];
+      if (cond && EPI != VITS_EPI_UPSAMPLE) e += cond[idx];
+    }
+    erow[tid] = e;
+  }
+  __syncthreads();
+
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int n = n0 + wn + ni * 32 + l32;
+      const int rloc = wm + mi * 32 + 4 * lhi;  // tile-local row of register 0
+      const int rbase = m0 + rloc;
+      if (EPI == VITS_EPI_GATE) {
+        // packed rows 2q (tanh half) / 2q+1 (sigmoid half) live in the same
+        // lane in registers r, r+1 (r even): no cross-lane traffic.
+        if (n < p.n_out) {
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const int ro = (r & 3) + 8 * (r >> 2);
+            const int row = rbase + ro;
+            if (row < p.m) {
+              const float va = acc[mi][ni][r] + erow[rloc + ro];
+              const float vb = acc[mi][ni][r + 1] + erow[rloc + ro + 1];
+              const float v = fast_tanh(va) * fast_sigmoid(vb);
+              store_std(o0, b, row >> 1, n, v, n >= len_b);
+            }
+          }
+        }
+      } else if (EPI == VITS_EPI_UPSAMPLE) {
+        const int u = p.up_u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const int row = rbase + ro;
+          if (row < p.m && n < p.n_out) {
+            const int oc = row / u;
+            const int ph = row - oc * u;
+            const int t = n * u + ph - p.up_pad;
+            if (t >= 0 && t < p.t_out) {
+              const float v = acc[mi][ni][r] + erow[rloc + ro];
+              store_std(o0, b, oc, t, v, t >= len_b);
+            }
+          }
+        }
+      } else if (EPI == EPI_STORE2) {
+        OutDesc o1{p.out1.y, p.out1.y_bstride, p.out1.y_cstride, p.out1.act, p.out1.res,
+                   p.out1.res_bstride, p.out1.res_cstride, p.out1.res_scale,
+                   p.out1.accumulate, p.out1.post_div};
+        if (n < p.n_out) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ro = (r & 3) + 8 * (r >> 2);
+            const int row = rbase + ro;
+            if (row < p.m) {
+              const float v = acc[mi][ni][r] + erow[rloc + ro];
+              if (row < p.split)
+                store_std(o0, b, row, n, v, n >= len_b);
+              else
+                store_std(o1, b, row - p.split, n, v, n >= len_b);
+            }
+          }
+        }
+      } else {
+        // single-output STORE: every residual / accumulator load of this
+        // 32x32 sub-tile is issued before the first store, so the 16 round
+        // trips overlap (res may alias y: each element is still read before
+        // it is written, by the same lane).
+        if (n < p.n_out) {
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            v[r] = apply_act(acc[mi][ni][r] + erow[rloc + (r & 3) + 8 * (r >> 2)], o0.act);
+          float* yb = o0.y + (int64_t)b * o0.y_bstride + n;
+          if (o0.res) {
+            const float* rb = o0.res + (int64_t)b * o0.res_bstride + n;
+            float rv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + (r & 3) + 8 * (r >> 2);
+              rv[r] = rb[(int64_t)(row < p.m ? row : 0) * o0.res_cstride];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = rv[r] + o0.res_scale * v[r];
+          }
+          if (o0.accumulate) {
+            float yo[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + (r & 3) + 8 * (r >> 2);
+              yo[r] = yb[(int64_t)(row < p.m ? row : 0) * o0.y_cstride];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = yo[r] + v[r];
+          }
+          const bool msk = n >= len_b;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + (r & 3) + 8 * (r >> 2);
+            float t = v[r];
+            if (o0.post_div != 1.0f) t = t / o0.post_div;
+            if (msk) t = 0.f;
+            if (row < p.m) yb[(int64_t)row * o0.y_cstride] = t;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM_, int WN_, int WT, bool V4>
+int launch_tile_v(const vits_conv1d_desc& d, int batch, hipStream_t s, size_t xrs) {
+  constexpr bool BF = WT != VITS_WDT_F32;
+  const size_t wsz = BF ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
+  const size_t xsz = (size_t)d.kc * xrs;
+  if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) || xsz > (size_t)XTile<BN, BF>::floats)
+    return VITS_E_UNSUP;
+  // 32-bit window offsets
+  if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
+    return VITS_E_UNSUP;
+  const size_t xslots = BF ? (xrs * (d.kc + 4) + 1) / 2 : xsz;
+  // + tail pad: the software pipeline reads one k-step past the last chunk
+  const size_t lds = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xrs + 64);
+  dim3 grid((d.n_out + BN - 1) / BN, (d.m + BM - 1) / BM, batch);
+  dim3 block(256);
+  switch (d.epi) {
+    case VITS_EPI_STORE:
+      if (d.split < d.m)
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, WT, V4>), grid, block, lds, s, d);
+      else
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, WT, V4>), grid, block, lds, s, d);
+      break;
+    case VITS_EPI_GATE:
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, WT, V4>), grid, block, lds, s, d);
+      break;
+    case VITS_EPI_UPSAMPLE:
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, WT, V4>), grid, block, lds, s, d);
+      break;
+    default:
+      return VITS_E_UNSUP;
+  }
+  return vits_launch_status();
+}
+
+// 16-byte X staging when every window row is a 16-byte-aligned run of time
+// steps (the [B][C][T] activations with T % 4 == 0) and the wider window
+// still fits the stage; element-wise staging otherwise
+template <int BM, int BN, int WM_, int WN_, int WT>
+int launch_tile(const vits_conv1d_desc& d, int batch, hipStream_t s) {
+  constexpr bool BF = WT != VITS_WDT_F32;
+  const int xw = BN + (d.k - 1) * d.dil;
+  const int xw_pad = (xw + 3) & ~3;
+  const int xsh = (d.pad_left & 3) ? 4 - (d.pad_left & 3) : 0;
+  const int xrs4 = 4 * ((xw + xsh + 3) >> 2);
+  const bool v4 = d.x_tstride == 1 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
+                  (d.tin & 3) == 0 && d.pad_left >= 0 &&
+                  (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
+                  (size_t)d.kc * xrs4 <= (size_t)XTile<BN, BF>::floats;
+  if (v4) return launch_tile_v<BM, BN, WM_, WN_, WT, true>(d, batch, s, xrs4);
+  return launch_tile_v<BM, BN, WM_, WN_, WT, false>(d, batch, s, xw_pad);
+}
+
+template <int WT>
+int conv1d_dispatch(const vits_conv1d_desc& d, int batch, hipStream_t s) {
+  constexpr bool BF = WT != VITS_WDT_F32;
+  switch (d.tile) {
+    case VITS_TILE_128x128: {
+      // a 128x128 grid that cannot fill the chip twice over (256 CUs) runs
+      // as 64x128 tiles: same packing (its W/X budgets are a subset), twice
+      // the workgroups
+      const long blocks = (long)((d.n_out + 127) / 128) * ((d.m + 127) / 128) * batch;
+      if (blocks < 512) return launch_tile<64, 128, 2, 2, WT>(d, batch, s);
+      return launch_tile<128, 128, 2, 2, WT>(d, batch, s);
+    }
+    case VITS_TILE_64x128:
+      return launch_tile<64, 128, 2, 2, WT>(d, batch, s);
+    case VITS_TILE_64x256: {
+      // same fallback for 64x256 grids (the flow / text-side convs at
+      // T ~ 500) when the chunk's input window also fits the 128-column tile
+      const long blocks = (long)((d.n_out + 255) / 256) * ((d.m + 63) / 64) * batch;
+      const int xw_pad128 = (128 + (d.k - 1) * d.dil + 3) & ~3;
+      if (blocks < 512 && d.kc * xw_pad128 <= XTile<128, BF>::floats)
+        return launch_tile<64, 128, 2, 2, WT>(d, batch, s);
+      return launch_tile<64, 256, 1, 4, WT>(d, batch, s);
+    }
+    case VITS_TILE_32x256:
+      return launch_tile<32, 256, 1, 4, WT>(d, batch, s);
+    default:
+      return VITS_E_UNSUP;
+  }
+}
+
+}  // namespace vits_conv
+
+// per-type entry points (defined in conv1d_{f32,bf16,f16}.hip)
+int vits_conv1d_dispatch_f32(const vits_conv1d_desc& d, int batch, hipStream_t s);
+int vits_conv1d_dispatch_bf16(const vits_conv1d_desc& d, int batch, hipStream_t s);
+int vits_conv1d_dispatch_f16(const vits_conv1d_desc& d, int batch, hipStream_t s);

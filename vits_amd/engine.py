@@ -50,10 +50,13 @@ def get_plan(module: torch.nn.Module, builder):
     sig = _param_signature(module)
     plan = module.__dict__.get(_PLAN_ATTR)
     if plan is None or plan.signature != sig:
-        # a bf16 model runs its convs on the bf16-MFMA kernel variant (fp32
-        # activations, fp32 accumulation); fp32 and fp16 models run exact fp32
-        lowp = sig[0] is not None and sig[0][2] == torch.bfloat16
-        with torch.no_grad(), ops.pack_bf16(lowp):
+        # a bf16 / fp16 model (`model.to(torch.bfloat16)`, `model.half()` as
+        # infer.py deploys) runs its convs on the 16-bit-MFMA kernel variant of
+        # its own type (fp32 activations, fp32 accumulation); fp32 models run
+        # exact fp32
+        dt = sig[0][2] if sig[0] is not None else torch.float32
+        wdt = {torch.bfloat16: ops.WDT_BF16, torch.float16: ops.WDT_F16}.get(dt, ops.WDT_F32)
+        with torch.no_grad(), ops.pack_lowp(wdt):
             plan = builder(module)
         plan.signature = sig
         module.__dict__[_PLAN_ATTR] = plan

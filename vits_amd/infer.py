@@ -2,8 +2,8 @@
 
 Same constructor and ``infer`` contract as ``infer.py:12-184``: speaker-id
 mapping files ``*.map``, per-speaker emotion banks ``{spk}.emo`` next to the
-checkpoint, an fp16 model (``.half()`` like the reference; the HIP plans
-compute in fp32 internally and hand back the model dtype), a fixed noise
+checkpoint, an fp16 model (``.half()`` like the reference: its convs run on
+the fp16-MFMA kernel variant with fp32 accumulation), a fixed noise
 buffer sliced at a random offset per call.  Differences: the noise buffer
 lives on the device (no host->device copy per call) and the CLI writes WAVs
 with scipy instead of soundfile.

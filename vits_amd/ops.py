@@ -16,7 +16,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, WDT_BF16, WDT_F32, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
+from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
                    EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS,
                    check)
 
@@ -138,15 +138,15 @@ class PackedConv:
     up_pad: int = 0
     out_channels: int = 0      # channels of the produced tensor
     extra: dict = field(default_factory=dict)
-    wdtype: int = WDT_F32      # WDT_BF16: w is [cin_pad/kc][k][kc/8][m_pad][8] bf16
+    wdtype: int = WDT_F32      # WDT_BF16 / WDT_F16: w is [cin_pad/kc][k][kc/8][m_pad][8] 16-bit
 
     @property
     def m_pad(self) -> int:
-        return self.w.shape[3] if self.wdtype == WDT_BF16 else self.w.shape[2]
+        return self.w.shape[3] if self.wdtype != WDT_F32 else self.w.shape[2]
 
     @property
     def cin_pad(self) -> int:
-        return self.w.shape[0] * self.kc if self.wdtype == WDT_BF16 else self.w.shape[0]
+        return self.w.shape[0] * self.kc if self.wdtype != WDT_F32 else self.w.shape[0]
 
 
 def _finish_pack(rows_w: torch.Tensor, k: int, tile: int, dil: int = 1) -> tuple[torch.Tensor, int]:
@@ -161,29 +161,36 @@ def _finish_pack(rows_w: torch.Tensor, k: int, tile: int, dil: int = 1) -> tuple
 
 
 class _PackPrecision(threading.local):
-    bf16 = False
+    wdtype = WDT_F32
 
 
 PACK_PRECISION = _PackPrecision()
+_WDT_TORCH = {WDT_BF16: torch.bfloat16, WDT_F16: torch.float16}
 
 
 @contextlib.contextmanager
-def pack_bf16(enabled: bool = True):
-    """While active, pack_conv / pack_conv_transpose return bf16-MFMA layers
-    (engine plans of a bf16 model are built under it)."""
-    old = PACK_PRECISION.bf16
-    PACK_PRECISION.bf16 = bool(enabled)
+def pack_lowp(wdtype: int = WDT_BF16):
+    """While active, pack_conv / pack_conv_transpose return 16-bit-MFMA layers
+    (WDT_BF16 or WDT_F16; WDT_F32 = exact fp32).  Engine plans of a bf16 /
+    fp16 model are built under it."""
+    old = PACK_PRECISION.wdtype
+    PACK_PRECISION.wdtype = int(wdtype)
     try:
         yield
     finally:
-        PACK_PRECISION.bf16 = old
+        PACK_PRECISION.wdtype = old
 
 
-def to_bf16(layer: PackedConv) -> PackedConv:
-    """Re-pack an fp32 layer for the bf16-MFMA kernel variant: K-chunks of 16
-    channels, W as [cin_pad/16][k][2][m_pad][8] bf16 (one 16-byte A fragment
-    per row and 8 channels), tile by _pick_tile_bf16."""
-    if layer.wdtype == WDT_BF16:
+def pack_bf16(enabled: bool = True):
+    return pack_lowp(WDT_BF16 if enabled else WDT_F32)
+
+
+def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
+    """Re-pack an fp32 layer for the 16-bit-MFMA kernel variant (bf16 or
+    fp16 operands, fp32 accumulation): K-chunks of 16 channels, W as
+    [cin_pad/16][k][2][m_pad][8] (one 16-byte A fragment per row and 8
+    channels), tile by _pick_tile_bf16."""
+    if layer.wdtype != WDT_F32 or wdtype == WDT_F32:
         return layer
     kc = 16
     w32 = layer.w[:layer.cin]                          # [cin, k, m_pad]
@@ -193,9 +200,14 @@ def to_bf16(layer: PackedConv) -> PackedConv:
     w[:layer.cin] = w32
     w = w.view(cin_pad // kc, kc // 8, 8, k, m_pad).permute(0, 3, 1, 4, 2).contiguous()
     tile = _pick_tile_bf16(layer.m, layer.k)
-    return PackedConv(w.to(torch.bfloat16), layer.bias, layer.cin, layer.m, layer.k, layer.dil,
-                      layer.pad_left, layer.epi, tile, kc, up_u=layer.up_u, up_pad=layer.up_pad,
-                      out_channels=layer.out_channels, extra=layer.extra, wdtype=WDT_BF16)
+    return PackedConv(w.to(_WDT_TORCH[wdtype]), layer.bias, layer.cin, layer.m, layer.k,
+                      layer.dil, layer.pad_left, layer.epi, tile, kc, up_u=layer.up_u,
+                      up_pad=layer.up_pad, out_channels=layer.out_channels, extra=layer.extra,
+                      wdtype=wdtype)
+
+
+def to_bf16(layer: PackedConv) -> PackedConv:
+    return to_lowp(layer, WDT_BF16)
 
 
 def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], *, dilation: int = 1,
@@ -218,7 +230,7 @@ def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], *, dilation: i
     b = None if bias is None else bias.detach().to(torch.float32).contiguous()
     layer = PackedConv(packed, b, cin, cout, k, dilation, padding, epi, tile, kc,
                        out_channels=outc)
-    return to_bf16(layer) if PACK_PRECISION.bf16 else layer
+    return to_lowp(layer, PACK_PRECISION.wdtype)
 
 
 def pack_conv_transpose(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
@@ -240,7 +252,7 @@ def pack_conv_transpose(weight: torch.Tensor, bias: Optional[torch.Tensor], stri
     b = None if bias is None else bias.detach().to(torch.float32).contiguous()
     layer = PackedConv(packed, b, cin, cout * u, kp, 1, kp - 1, EPI_UPSAMPLE, tile, kc,
                        up_u=u, up_pad=padding, out_channels=cout)
-    return to_bf16(layer) if PACK_PRECISION.bf16 else layer
+    return to_lowp(layer, PACK_PRECISION.wdtype)
 
 
 # ---------------------------------------------------------------------------
