@@ -271,31 +271,47 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
       // fp32 X window at column n + j*dil, rounded to bf16 in registers
       const char* wbytes = reinterpret_cast<const char*>(ws);
       const int c8n = kc >> 3;
-      for (int j = 0; j < k; ++j) {
-        for (int g = 0; g < (kc >> 4); ++g) {
-          lpx8 a[TM], bb[TN];
+      const int G = kc >> 4;       // 16-channel groups per tap
+      const int nsteps = k * G;    // k-steps of this chunk, (j, g) with g fastest
+      auto load = [&](int st, lpx8* a, lpx8* bb) {
+        const int j = st / G;
+        const int g = st - j * G;
 #pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
-            a[mi] = *reinterpret_cast<const lpx8*>(
-                wbytes + ((int64_t)((j * c8n + 2 * g + lhi) * BM + wm + mi * 32 + l32) << 4));
+        for (int mi = 0; mi < TM; ++mi)
+          a[mi] = *reinterpret_cast<const lpx8*>(
+              wbytes + ((int64_t)((j * c8n + 2 * g + lhi) * BM + wm + mi * 32 + l32) << 4));
 #pragma unroll
-          for (int ni = 0; ni < TN; ++ni) {
-            const lp_t* xp = reinterpret_cast<const lp_t*>(xs) +
-                               (wn + ni * 32 + l32 + j * dil + xsh) * kcp + 16 * g + 8 * lhi;
-            const lpx4 lo = *reinterpret_cast<const lpx4*>(xp);
-            const lpx4 hi = *reinterpret_cast<const lpx4*>(xp + 4);
-            bb[ni] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          }
-#pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < TN; ++ni)
-              if constexpr (WT == VITS_WDT_F16)
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
-              else
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
+        for (int ni = 0; ni < TN; ++ni) {
+          const lp_t* xp = reinterpret_cast<const lp_t*>(xs) +
+                           (wn + ni * 32 + l32 + j * dil + xsh) * kcp + 16 * g + 8 * lhi;
+          const lpx4 lo = *reinterpret_cast<const lpx4*>(xp);
+          const lpx4 hi = *reinterpret_cast<const lpx4*>(xp + 4);
+          bb[ni] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         }
+      };
+      auto mma = [&](const lpx8* a, const lpx8* bb) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            if constexpr (WT == VITS_WDT_F16)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
+            else
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
+      };
+      // two register sets: the fragments of step s+1 are read under the
+      // MFMAs of step s (the read past the last step stays inside the
+      // stage's padded LDS and is never consumed)
+      lpx8 a0[TM], b0[TN], a1[TM], b1[TN];
+      load(0, a0, b0);
+      int st = 0;
+      for (; st + 2 <= nsteps; st += 2) {
+        load(st + 1, a1, b1);
+        mma(a0, b0);
+        load(st + 2, a0, b0);
+        mma(a1, b1);
       }
+      if (st < nsteps) mma(a0, b0);
     } else {
       // k-step s = (tap j, channel pair cp), cp fastest: A rows (2cp + lhi)*k + j
       // of W, B row 2cp + lhi of X shifted by j*dil.  Two register sets ping-
