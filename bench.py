@@ -103,7 +103,7 @@ def cpu_baseline(model, Tx, Ty, budget_s=12.0):
             V.infer_p2(sd, attn, m_p, s_p, g, noise, BASE_MODEL)
             n += 1
             el = time.perf_counter() - t0
-            if el >= budget_s or n >= 50:
+            if el >= budget_s or n >= 400:
                 break
     samples = n * Ty * HOP
     return {"value": samples / el, "unit": "output samples/s", "cores": cores, "kind": "port",
