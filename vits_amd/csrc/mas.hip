@@ -31,7 +31,13 @@
 
 namespace {
 
-constexpr int MAS_R = 16;                 // rows per streamed chunk
+// rows per streamed chunk: as many as keep the two ring buffers within
+// MAS_RING_BYTES, so wave 0's compute per chunk outlasts one HBM round trip
+constexpr int MAS_RING_BYTES = 64 * 1024;
+__host__ __device__ inline int mas_rows(int xpl) {
+  int r = MAS_RING_BYTES / (2 * 64 * xpl * (int)sizeof(float));
+  return r > 64 ? 64 : (r < 4 ? 4 : r);
+}
 constexpr float MAS_NEG = -1e9f;
 constexpr int MAS_BITS_LDS_MAX = 48 * 1024;
 
@@ -84,7 +90,7 @@ __global__ __launch_bounds__(64) void mas_lengths_kernel(const void* mask, int d
   }
 }
 
-template <int XPL>
+template <int XPL, bool BITS_LDS>
 __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_cent,
                                                   const int32_t* __restrict__ tt_len,
                                                   const int32_t* __restrict__ ts_len, void* path,
@@ -98,11 +104,17 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
   const int wid = tid >> 6;
   const int W = 64 * XPL;  // padded row width in LDS (>= T_s)
 
-  float* ring = reinterpret_cast<float*>(smem_raw);                 // [2][R][W]
-  int32_t* idx_row = reinterpret_cast<int32_t*>(ring + 2 * MAS_R * W);  // [T_t]
-  uint64_t* bits = bits_in_lds
-                       ? reinterpret_cast<uint64_t*>(idx_row + ((T_t + 1) & ~1))
-                       : bits_global + (int64_t)b * T_t * XPL;
+  const int R = mas_rows(XPL);
+  float* ring = reinterpret_cast<float*>(smem_raw);             // [2][R][W]
+  int32_t* idx_row = reinterpret_cast<int32_t*>(ring + 2 * R * W);  // [T_t]
+  // compile-time address space for the decision bits: LDS (ds_read/write)
+  // or the global workspace -- a runtime select would make every access a
+  // FLAT op waiting on both counters
+  uint64_t* bits;
+  if constexpr (BITS_LDS)
+    bits = reinterpret_cast<uint64_t*>(idx_row + ((T_t + 1) & ~1));
+  else
+    bits = bits_global + (int64_t)b * T_t * XPL;
 
   int t_t = tt_len[b];
   int t_s = ts_len[b];
@@ -110,20 +122,28 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
   t_s = t_s < 0 ? 0 : (t_s > T_s ? T_s : t_s);
 
   const float* nc = neg_cent + (int64_t)b * T_t * T_s;
-  const int nchunks = (t_t + MAS_R - 1) / MAS_R;
+  const int nchunks = (t_t + R - 1) / R;
 
-  auto load_chunk = [&](int ch, int buf, int t0, int nthr) {
-    float* dst = ring + buf * MAS_R * W;
-    const int y0 = ch * MAS_R;
-    for (int i = t0; i < MAS_R * W; i += nthr) {
-      const int r = i / W;
-      const int x = i - r * W;
-      const int y = y0 + r;
-      dst[i] = (y < t_t && x < t_s) ? nc[(int64_t)y * T_s + x] : 0.f;
+  // chunk -> LDS by LDS-DMA (4 bytes per lane, 64 floats per wave
+  // instruction, all in flight at once; no registers, no per-load waits).
+  // Columns >= t_s and rows >= t_t read clamped in-bounds addresses: the DP
+  // never uses them (x < hi <= t_s, y < t_t).
+  auto load_chunk = [&](int ch, int buf, int w0, int nw) {
+    float* dst = ring + buf * R * W;
+    const int y0 = ch * R;
+    const int pieces = R * W / 64;
+    for (int q = (tid >> 6) - w0; q < pieces; q += nw) {
+      const int r = (q * 64) / W;
+      const int x = q * 64 - r * W + (tid & 63);
+      const int y = min(y0 + r, T_t - 1);
+      const int xc = min(x, T_s - 1);
+      __builtin_amdgcn_global_load_lds(nc + (int64_t)y * T_s + xc,
+                                       (__attribute__((address_space(3))) void*)(dst + q * 64),
+                                       4, 0, 0);
     }
   };
 
-  if (nchunks > 0) load_chunk(0, 0, tid, 256);
+  if (nchunks > 0) load_chunk(0, 0, 0, 4);
   __syncthreads();
 
   float vp[XPL];
@@ -133,19 +153,32 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
 
   for (int ch = 0; ch < nchunks; ++ch) {
     if (wid != 0) {
-      if (ch + 1 < nchunks) load_chunk(ch + 1, (ch + 1) & 1, tid - 64, 192);
+      if (ch + 1 < nchunks) load_chunk(ch + 1, (ch + 1) & 1, 1, 3);
     } else {
-      const float* rows = ring + (ch & 1) * MAS_R * W;
-      const int y0 = ch * MAS_R;
-      const int yend = min(t_t, y0 + MAS_R);
+      const float* rows = ring + (ch & 1) * R * W;
+      const int y0 = ch * R;
+      const int yend = min(t_t, y0 + R);
+      // the next row's scores are read from LDS while this row computes
+      float nxt[XPL];
+      if (y0 < yend) {
+#pragma unroll
+        for (int i = 0; i < XPL; ++i) nxt[i] = rows[xbase + i];
+      }
       for (int y = y0; y < yend; ++y) {
-        const float* row = rows + (y - y0) * W + xbase;
         float cur[XPL];
 #pragma unroll
-        for (int i = 0; i < XPL; ++i) cur[i] = row[i];
+        for (int i = 0; i < XPL; ++i) cur[i] = nxt[i];
+        if (y + 1 < yend) {
+          const float* rown = rows + (y + 1 - y0) * W + xbase;
+#pragma unroll
+          for (int i = 0; i < XPL; ++i) nxt[i] = rown[i];
+        }
         const int lo = max(0, t_s + y - t_t);
         const int hi = min(t_s, y + 1);
-        const float left = __shfl_up(vp[XPL - 1], 1, 64);
+        // column x-1 of this lane's first element: lane-1's last register,
+        // one DPP wave shift (no LDS round trip; lane 0 never uses it)
+        const float left = __int_as_float(
+            __builtin_amdgcn_update_dpp(0, __float_as_int(vp[XPL - 1]), 0x138, 0xf, 0xf, false));
         float vn[XPL];
 #pragma unroll
         for (int i = 0; i < XPL; ++i) {
@@ -191,12 +224,12 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
   __syncthreads();
 
   // ---- write the full path tile ---------------------------------------------
+  // one wave per row, lanes along the row: coalesced, no index division
   const int64_t pbase = (int64_t)b * T_t * T_s;
-  for (int64_t i = tid; i < (int64_t)T_t * T_s; i += 256) {
-    const int y = (int)(i / T_s);
-    const int x = (int)(i - (int64_t)y * T_s);
-    const float v = (y < t_t && t_s > 0 && x == idx_row[y]) ? 1.f : 0.f;
-    store_dt(path, path_dt, pbase + i, v);
+  for (int y = wid; y < T_t; y += 4) {
+    const int sel = (y < t_t && t_s > 0) ? idx_row[y] : -1;
+    const int64_t rbase = pbase + (int64_t)y * T_s;
+    for (int x = lane; x < T_s; x += 64) store_dt(path, path_dt, rbase + x, x == sel ? 1.f : 0.f);
   }
 }
 
@@ -213,7 +246,7 @@ int mas_run(const float* neg_cent, const int32_t* tt, const int32_t* ts, void* p
             int batch, int T_t, int T_s, void* workspace, int64_t ws_bytes, hipStream_t s) {
   const int xpl = pick_xpl(T_s);
   if (xpl > 32) return VITS_E_UNSUP;
-  const size_t ring = sizeof(float) * 2 * MAS_R * 64 * xpl;
+  const size_t ring = sizeof(float) * 2 * mas_rows(xpl) * 64 * xpl;
   const size_t idx = sizeof(int32_t) * ((T_t + 1) & ~1);
   const size_t bb = bits_bytes(T_t, xpl);
   int in_lds = bb <= (size_t)MAS_BITS_LDS_MAX && ring + idx + bb <= 150 * 1024;
@@ -225,10 +258,14 @@ int mas_run(const float* neg_cent, const int32_t* tt, const int32_t* ts, void* p
   }
   if (lds > 160 * 1024) return VITS_E_UNSUP;
   dim3 grid(batch), block(256);
-#define MAS_CASE(X)                                                                              \
-  case X:                                                                                        \
-    hipLaunchKernelGGL(mas_kernel<X>, grid, block, lds, s, neg_cent, tt, ts, path, path_dt, T_t, \
-                       T_s, gbits, in_lds);                                                      \
+#define MAS_CASE(X)                                                                         \
+  case X:                                                                                   \
+    if (in_lds)                                                                             \
+      hipLaunchKernelGGL((mas_kernel<X, true>), grid, block, lds, s, neg_cent, tt, ts, path, \
+                         path_dt, T_t, T_s, gbits, in_lds);                                 \
+    else                                                                                    \
+      hipLaunchKernelGGL((mas_kernel<X, false>), grid, block, lds, s, neg_cent, tt, ts, path, \
+                         path_dt, T_t, T_s, gbits, in_lds);                                 \
     break;
   switch (xpl) {
     MAS_CASE(1)
@@ -249,7 +286,7 @@ int mas_run(const float* neg_cent, const int32_t* tt, const int32_t* ts, void* p
 extern "C" int64_t vits_maximum_path_workspace(int batch, int t_t, int t_s) {
   if (batch <= 0 || t_t <= 0 || t_s <= 0) return 0;
   const int xpl = pick_xpl(t_s);
-  const size_t ring = sizeof(float) * 2 * MAS_R * 64 * xpl;
+  const size_t ring = sizeof(float) * 2 * mas_rows(xpl) * 64 * xpl;
   const size_t idx = sizeof(int32_t) * ((t_t + 1) & ~1);
   const size_t bb = bits_bytes(t_t, xpl);
   const bool in_lds = bb <= (size_t)MAS_BITS_LDS_MAX && ring + idx + bb <= 150 * 1024;
