@@ -349,21 +349,25 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   #pragma unroll
         for (int ni = 0; ni < TN; ++ni) b1[ni] = pb[ni * 32];
         advance();
+        __builtin_amdgcn_s_setprio(1);
   #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
   #pragma unroll
           for (int ni = 0; ni < TN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
   #pragma unroll
         for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
   #pragma unroll
         for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
         advance();
+        __builtin_amdgcn_s_setprio(1);
   #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
   #pragma unroll
           for (int ni = 0; ni < TN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[mi], b1[ni], acc[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
       }
       if (s < steps) {
   #pragma unroll
