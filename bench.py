@@ -251,6 +251,52 @@ def kernels_leg(device):
     }
 
 
+def train_cpu_baseline(steps=2, B=4):
+    """The same train_stft step on the host cores (BASELINE.md measured the
+    reference at B=4 on 8 vCPU): vits_amd.train.TrainStep on CPU with the
+    three HIP-only ops swapped for CPU restatements -- MAS from
+    oracle/mas_oracle.c, neg_cent from oracle/vits_oracle.py, STFT magnitude
+    from torch.stft -- i.e. the reference algorithm in PyTorch-CPU fp32."""
+    import vits_amd.models as vm
+    from vits_amd import ops
+    from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
+    from oracle import mas as mas_oracle
+    from oracle.vits_oracle import neg_cent as nc_oracle
+
+    def cpu_mas(neg_cent, mask):
+        p = mas_oracle.maximum_path(neg_cent.detach().float().numpy(), mask.detach().float().numpy())
+        return torch.from_numpy(p).to(dtype=neg_cent.dtype)
+
+    def cpu_nc(z, m, lg):
+        return nc_oracle(z.detach().float(), m.detach().float(), lg.detach().float())
+
+    def cpu_stft(x, window, n_fft, hop, win, pad=None, eps=1e-7):
+        spec = torch.stft(x.float(), n_fft, hop, win, window, center=True, pad_mode="reflect",
+                          return_complex=True)
+        return torch.sqrt(spec.real ** 2 + spec.imag ** 2 + eps)
+
+    saved = (vm.maximum_path, vm.neg_cent_scores, ops.stft_mag)
+    vm.maximum_path, vm.neg_cent_scores, ops.stft_mag = cpu_mas, cpu_nc, cpu_stft
+    try:
+        hps = default_hps()
+        torch.manual_seed(hps.train.seed)
+        dev = torch.device("cpu")
+        g, d = build_models(hps, dev)
+        st = TrainStep(hps, g, d, dev, log_mels=False)
+        batch = synthetic_batch(hps, B, seed=0)
+        st.step(batch)  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st.step(batch)
+        el = time.perf_counter() - t0
+    finally:
+        vm.maximum_path, vm.neg_cent_scores, ops.stft_mag = saved
+    return {"value": round(B * steps / el, 3), "unit": "utt/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{steps} x train_stft step B={B} Tx=100 Ty=500 fp32 on CPU in {el:.1f} s "
+                      "(vits_amd.train.TrainStep, MAS/neg_cent from oracle/, torch.stft)"}
+
+
 def train_leg(args, device, rank, world, dist):
     """Timed train_stft steps (BASELINE C3/C4) on synthetic base.json batches."""
     from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
@@ -289,6 +335,8 @@ def train_leg(args, device, rank, world, dist):
            "tflops_alg": round(365.4e9 * utt / el / 1e12, 2),
            "loss_gen_all": round(float(out["loss_gen_all"]), 4),
            "reference_cpu": "0.945 utt/s at B=4 on 8 vCPU (BASELINE.md, measured in the survey)"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = train_cpu_baseline()
     del st, net_g, net_d
     torch.cuda.empty_cache()
     return res
