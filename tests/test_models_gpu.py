@@ -241,3 +241,18 @@ def test_lowp_model_infer_p2_vs_reference(device, dt, min_snr):
     assert snr >= min_snr
     plan = m.dec.__dict__.get("_vits_amd_plan")
     assert plan is not None and plan.conv_pre.wdtype == {torch.bfloat16: 1, torch.float16: 2}[dt]
+
+
+def test_infer_p1_graph_matches_eager(base, device):
+    """capture_infer_p1 (per-length hipGraph used by EmoVITS) replays the same
+    kernels: bit-identical to eager infer_p1, also after new inputs."""
+    g = torch.Generator().manual_seed(21)
+    run = base.capture_infer_p1(37)
+    for _ in range(2):
+        x = torch.randn(1, 37, 256, generator=g).to(device)
+        emo = torch.randn(1, 1024, generator=g).to(device)
+        sid = torch.tensor([int(torch.randint(0, 2048, (1,), generator=g))], device=device)
+        ref = base.infer_p1(x, emo, sid)
+        got = run(x, emo, sid)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)

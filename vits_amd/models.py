@@ -273,6 +273,7 @@ class SynthesizerTrn(nn.Module):
         assert len(dilation_rate) == n_flows
         assert n_speakers > 1
         self.segment_size = segment_size
+        self.text_channels = text_channels
         self.inter_channels = inter_channels
         self.align_noise = align_noise
         self.align_noise_decay = align_noise_decay
@@ -428,6 +429,42 @@ class SynthesizerTrn(nn.Module):
         return o.to(m_p.dtype)
 
     # ------------------------------------------------------------ hipGraphs
+    @torch.no_grad()
+    def capture_infer_p1(self, t_x, warmup=2):
+        """Capture infer_p1 for one utterance of t_x tokens into a hipGraph
+        (the text side is ~55 small launches whose host-side descriptor
+        building dominates its B=1 latency).  Returns a callable(x, emo, sid)
+        -> (m_p, s_p, logw, g) reading / returning static buffers."""
+        dev = next(self.parameters()).device
+        dt = next(self.parameters()).dtype
+        static = dict(x=torch.zeros(1, t_x, self.text_channels, device=dev, dtype=dt),
+                      emo=torch.zeros(1, 1024, device=dev, dtype=dt),
+                      sid=torch.zeros(1, device=dev, dtype=torch.long))
+
+        def body():
+            return self.infer_p1(static["x"], static["emo"], static["sid"])
+
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                body()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = body()
+
+        def run(x, emo, sid):
+            static["x"].copy_(x)
+            static["emo"].copy_(emo)
+            static["sid"].copy_(sid)
+            graph.replay()
+            return out
+
+        run.graph = graph
+        run.static = static
+        return run
+
     @torch.no_grad()
     def capture_infer_p2(self, batch, t_x, t_y, warmup=2):
         """Capture infer_p2 for a static shape into a hipGraph (torch.cuda.CUDAGraph
