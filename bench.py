@@ -237,9 +237,12 @@ def kernels_leg(device):
     loss = MultiResolutionSTFTLoss().to(device)
     y = (torch.randn(B, L, generator=g) * 0.1).to(device)
     yh = (torch.randn(B, L, generator=g) * 0.1).to(device).requires_grad_(True)
-    fwd_ms = _event_ms(lambda: [f.mag(y) for f in loss.stft_losses])
+    specs = [(f.window, f.fft_size, f.hop_size, f.win_size, None, 1e-7) for f in loss.stft_losses]
+    yd = yh.detach()
+    # the loss's forward: both signals x 5 resolutions in one launch
+    fwd_ms = _event_ms(lambda: ops.stft_mag_multi([y] * 5 + [yd] * 5, specs + specs))
     mags = sum((f.fft_size // 2 + 1) * (L // f.hop_size + 1) for f in loss.stft_losses)
-    fwd_bytes = B * (len(loss.stft_losses) * L * 4 + mags * 4)
+    fwd_bytes = 2 * B * (len(loss.stft_losses) * L * 4 + mags * 4)
 
     def fb():
         sc, mg, _, _ = loss(yh, y)
@@ -257,7 +260,7 @@ def kernels_leg(device):
                      "shape": f"B={B} C={C} t_t={Tt} t_s={Ts}"},
         "mrstft_mag_fwd": {"ms": round(fwd_ms, 4), "GBps": round(fwd_bytes / fwd_ms / 1e6, 1),
                            "frac_hbm": round(fwd_bytes / fwd_ms / 1e6 / peak, 4),
-                           "shape": f"B={B} L={L} x 5 resolutions (one signal)"},
+                           "shape": f"B={B} L={L} x 5 resolutions x 2 signals, one launch"},
         "mrstft_loss_fwd_bwd_ms": round(fb_ms, 4),
     }
 

@@ -30,7 +30,9 @@
  *   vits_conv_post_tanh      Generator tail: leaky_relu(0.01) -> conv_post
  *                            -> tanh (models.py:315-317)
  *   vits_stft_mag_forward /  TorchSTFT.stft + STFTLoss.spec2mag
- *   vits_stft_mag_backward   (modules.py:386-392, stft_loss.py:22-23)
+ *   vits_stft_mag_backward   (modules.py:386-392, stft_loss.py:22-23);
+ *   (_multi)                 all resolutions of MultiResolutionSTFTLoss
+ *                            (stft_loss.py:47-95) in one launch
  *   vits_layer_norm_channels modules.LayerNorm (modules.py:41-44)
  *   vits_attention_forward   MultiHeadAttention.attention core
  *                            (attentions.py:85-100)
@@ -213,6 +215,33 @@ int vits_stft_mag_backward(const float* grad_mag, const float* mag, const float*
                            int n_fft, int hop, int win, int pad, float* grad_x,
                            float* workspace, int64_t workspace_floats, void* stream);
 int64_t vits_stft_workspace(int batch, int length, int n_fft, int hop, int pad);
+
+/* Several transforms in one launch (the 2 signals x 5 resolutions of the */
+/* MR-STFT loss, stft_loss.py:47-95): up to 16 jobs, each with its own    */
+/* signal batch, resolution and outputs.  Forward uses x, window, sizes,  */
+/* eps, mag, re, im; backward uses grad_mag, mag, re, im, window, sizes,  */
+/* grad_x and a workspace of vits_stft_workspace_multi floats.            */
+typedef struct vits_stft_job {
+  const float* x;
+  const float* window;
+  const float* grad_mag;
+  float* mag;
+  float* re;
+  float* im;
+  float* grad_x;
+  int32_t batch;
+  int32_t length;
+  int32_t n_fft;
+  int32_t hop;
+  int32_t win;
+  int32_t pad;
+  float eps;
+  int32_t reserved;
+} vits_stft_job;
+int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs, void* stream);
+int vits_stft_mag_backward_multi(const vits_stft_job* jobs, int njobs, float* workspace,
+                                 int64_t workspace_floats, void* stream);
+int64_t vits_stft_workspace_multi(const vits_stft_job* jobs, int njobs);
 
 /* ---------------------------------------------------------------------- */
 /* channel LayerNorm over dim 1 of [B][C][T]:                             */

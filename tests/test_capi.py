@@ -40,14 +40,16 @@ def test_struct_layout_matches_header():
     import subprocess
     import tempfile
 
-    from vits_amd._lib import ConvDesc, ConvOut
+    from vits_amd._lib import ConvDesc, ConvOut, StftJob
 
     probe = r'''
 #include <stdio.h>
 #include <stddef.h>
 #include "vits_amd.h"
-int main(){printf("%zu %zu %zu %zu\n", sizeof(vits_conv1d_desc), sizeof(vits_conv_out),
- offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths)); return 0;}
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc), sizeof(vits_conv_out),
+ offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths),
+ offsetof(vits_conv1d_desc, wdtype), sizeof(vits_stft_job), offsetof(vits_stft_job, eps));
+ return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
         src = os.path.join(d, "p.c")
@@ -60,3 +62,6 @@ int main(){printf("%zu %zu %zu %zu\n", sizeof(vits_conv1d_desc), sizeof(vits_con
     assert int(out[1]) == ctypes.sizeof(ConvOut)
     assert int(out[2]) == ConvDesc.out0.offset
     assert int(out[3]) == ConvDesc.lengths.offset
+    assert int(out[4]) == ConvDesc.wdtype.offset
+    assert int(out[5]) == ctypes.sizeof(StftJob)
+    assert int(out[6]) == StftJob.eps.offset

@@ -342,3 +342,38 @@ def test_conv_transpose_bf16(device, dt):
         layer = ops.pack_conv_transpose(w.to(device), b.to(device), u, pad)
     out = ops.conv1d(x.to(device), layer, in_slope=0.1)
     _close(out, ref, tol=2e-5, what="bf16 convT")
+
+
+def test_stft_mag_multi_matches_single(device):
+    """The one-launch multi-job STFT (MR-STFT loss) equals the per-job kernel:
+    magnitudes bit for bit (same block code), input gradients to fp32
+    rounding (autograd sums the three per-resolution gradients of a signal
+    in its own order)."""
+    g = torch.Generator().manual_seed(3)
+    xs = [torch.randn(3, 9216, generator=g).to(device).requires_grad_(True) for _ in range(2)]
+    res = [(128, 32, 128), (512, 128, 512), (2048, 512, 2048)]
+    specs = [(torch.hann_window(w).to(device), n, h, w, None, 1e-7) for n, h, w in res]
+    mags = ops.stft_mag_multi([xs[0]] * 3 + [xs[1]] * 3, specs + specs)
+    loss = sum((m * (i + 1)).sum() for i, m in enumerate(mags))
+    gm = torch.autograd.grad(loss, xs)
+    xs1 = [x.detach().clone().requires_grad_(True) for x in xs]
+    ref = [ops.stft_mag(xs1[0], w, n, h, wl, eps=e) for (w, n, h, wl, _, e) in specs] + \
+          [ops.stft_mag(xs1[1], w, n, h, wl, eps=e) for (w, n, h, wl, _, e) in specs]
+    loss1 = sum((m * (i + 1)).sum() for i, m in enumerate(ref))
+    g1 = torch.autograd.grad(loss1, xs1)
+    for a, b in zip(mags, ref):
+        assert torch.equal(a, b)
+    for a, b in zip(gm, g1):
+        _close(a, b, tol=1e-6, what="multi-STFT grad")
+
+
+def test_stft_mag_multi_target_not_differentiable(device):
+    """Magnitudes of a signal without grad come back without a grad_fn (the
+    MR-STFT target), so a discriminator backward through them never reaches
+    the transform's backward."""
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 4096, generator=g).to(device).requires_grad_(True)
+    y = torch.randn(2, 4096, generator=g).to(device)
+    spec = (torch.hann_window(256).to(device), 256, 64, 256, None, 1e-7)
+    mx, my = ops.stft_mag_multi([x, y], [spec, spec])
+    assert mx.requires_grad and not my.requires_grad and my.grad_fn is None

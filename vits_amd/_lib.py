@@ -76,6 +76,26 @@ class ConvDesc(C.Structure):
     ]
 
 
+class StftJob(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p),
+        ("window", C.c_void_p),
+        ("grad_mag", C.c_void_p),
+        ("mag", C.c_void_p),
+        ("re", C.c_void_p),
+        ("im", C.c_void_p),
+        ("grad_x", C.c_void_p),
+        ("batch", C.c_int32),
+        ("length", C.c_int32),
+        ("n_fft", C.c_int32),
+        ("hop", C.c_int32),
+        ("win", C.c_int32),
+        ("pad", C.c_int32),
+        ("eps", C.c_float),
+        ("reserved", C.c_int32),
+    ]
+
+
 _SIGS = {
     "vits_conv1d_forward": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_void_p]),
     "vits_conv1d_forward_seq": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_int, C.c_void_p]),
@@ -104,6 +124,10 @@ _SIGS = {
          C.c_void_p, C.c_int64, C.c_void_p],
     ),
     "vits_maximum_path_workspace": (C.c_int64, [C.c_int, C.c_int, C.c_int]),
+    "vits_stft_mag_forward_multi": (C.c_int, [C.POINTER(StftJob), C.c_int, C.c_void_p]),
+    "vits_stft_mag_backward_multi": (
+        C.c_int, [C.POINTER(StftJob), C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),
+    "vits_stft_workspace_multi": (C.c_int64, [C.POINTER(StftJob), C.c_int]),
     "vits_neg_cent": (
         C.c_int,
         [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,

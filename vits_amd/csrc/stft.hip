@@ -72,85 +72,91 @@ __device__ float2* fft_lds(float2* a, float2* b, const float2* tw, int n, int lo
   return a;
 }
 
-__global__ __launch_bounds__(256) void stft_fwd_kernel(const float* __restrict__ x, int L,
-                                                       const float* __restrict__ window, int n,
-                                                       int log2n, int hop, int win, int pad,
-                                                       int frames, int fpb, float eps,
-                                                       float* __restrict__ mag,
-                                                       float* __restrict__ re,
-                                                       float* __restrict__ im) {
-  extern __shared__ float2 sfft[];
+// One transform job (a signal batch at one resolution), device side.
+struct StftJobD {
+  const float* x;       // forward input [B][L]
+  const float* window;  // [win]
+  const float* gmag;    // backward: d loss / d mag
+  float* mag;           // [B][n/2+1][frames]
+  float* re;
+  float* im;
+  float* dframes;       // backward workspace [B][frames][n]
+  float* gx;            // backward output [B][L]
+  int L, n, log2n, hop, win, pad, frames, fpb, batch;
+  float eps;
+};
+
+// forward: frames f0 .. f0+fpb-1 of utterance b
+__device__ void stft_fwd_block(const StftJobD& J, int fblk, int b, float2* sfft) {
+  const int n = J.n, fpb = J.fpb;
   float2* a = sfft;
   float2* bbuf = sfft + fpb * n;
   float2* tw = bbuf + fpb * n;
   fill_twiddles(tw, n);
-  const int b = blockIdx.y;
-  const int f0 = blockIdx.x * fpb;
-  const int woff = (n - win) / 2;
-  const float* xb = x + (int64_t)b * L;
+  const int f0 = fblk * fpb;
+  const int woff = (n - J.win) / 2;
+  const float* xb = J.x + (int64_t)b * J.L;
   for (int i = threadIdx.x; i < fpb * n; i += blockDim.x) {
     const int f = i / n;
     const int t = i - f * n;
     const int fr = f0 + f;
     float v = 0.f;
     const int wi = t - woff;
-    if (fr < frames && wi >= 0 && wi < win) {
-      const int src = reflect_idx(fr * hop + t - pad, L);
-      v = xb[src] * window[wi];
+    if (fr < J.frames && wi >= 0 && wi < J.win) {
+      const int src = reflect_idx(fr * J.hop + t - J.pad, J.L);
+      v = xb[src] * J.window[wi];
     }
     a[i] = make_float2(v, 0.f);
   }
   __syncthreads();
-  const float2* out = fft_lds(a, bbuf, tw, n, log2n, fpb, -1.f);
+  const float2* out = fft_lds(a, bbuf, tw, n, J.log2n, fpb, -1.f);
   const int nb = n / 2 + 1;
   for (int i = threadIdx.x; i < fpb * nb; i += blockDim.x) {
     const int k = i / fpb;
     const int f = i - k * fpb;
     const int fr = f0 + f;
-    if (fr >= frames) continue;
+    if (fr >= J.frames) continue;
     const float2 c = out[f * n + k];
-    const int64_t o = ((int64_t)b * nb + k) * frames + fr;
-    mag[o] = sqrtf(c.x * c.x + c.y * c.y + eps);
-    if (re) re[o] = c.x;
-    if (im) im[o] = c.y;
+    const int64_t o = ((int64_t)b * nb + k) * J.frames + fr;
+    J.mag[o] = sqrtf(c.x * c.x + c.y * c.y + J.eps);
+    if (J.re) J.re[o] = c.x;
+    if (J.im) J.im[o] = c.y;
   }
 }
 
-__global__ __launch_bounds__(256) void stft_bwd_frames_kernel(
-    const float* __restrict__ gmag, const float* __restrict__ mag, const float* __restrict__ re,
-    const float* __restrict__ im, const float* __restrict__ window, int n, int log2n, int win,
-    int frames, int fpb, float* __restrict__ dframes) {
-  extern __shared__ float2 sfft[];
+// backward, per frame: d mag / d(re, im) = (re, im) / mag, adjoint real DFT
+// = real part of the inverse FFT of the one-sided spectrum, windowed
+__device__ void stft_bwd_frames_block(const StftJobD& J, int fblk, int b, float2* sfft) {
+  const int n = J.n, fpb = J.fpb;
   float2* a = sfft;
   float2* bbuf = sfft + fpb * n;
   float2* tw = bbuf + fpb * n;
   fill_twiddles(tw, n);
-  const int b = blockIdx.y;
-  const int f0 = blockIdx.x * fpb;
+  const int f0 = fblk * fpb;
   const int nb = n / 2 + 1;
-  const int woff = (n - win) / 2;
+  const int woff = (n - J.win) / 2;
   for (int i = threadIdx.x; i < fpb * n; i += blockDim.x) {
     const int k = i / fpb;  // bin-major so reads along frames are contiguous
     const int f = i - k * fpb;
     const int fr = f0 + f;
     float2 g = make_float2(0.f, 0.f);
-    if (k < nb && fr < frames) {
-      const int64_t o = ((int64_t)b * nb + k) * frames + fr;
-      const float s = gmag[o] / mag[o];
-      g = make_float2(s * re[o], s * im[o]);
+    if (k < nb && fr < J.frames) {
+      const int64_t o = ((int64_t)b * nb + k) * J.frames + fr;
+      const float sc = J.gmag[o] / J.mag[o];
+      g = make_float2(sc * J.re[o], sc * J.im[o]);
     }
     a[f * n + k] = g;
   }
   __syncthreads();
-  const float2* out = fft_lds(a, bbuf, tw, n, log2n, fpb, +1.f);
+  const float2* out = fft_lds(a, bbuf, tw, n, J.log2n, fpb, +1.f);
   for (int i = threadIdx.x; i < fpb * n; i += blockDim.x) {
     const int f = i / n;
     const int t = i - f * n;
     const int fr = f0 + f;
-    if (fr >= frames) continue;
+    if (fr >= J.frames) continue;
     const int wi = t - woff;
-    const float w = (wi >= 0 && wi < win) ? window[wi] : 0.f;
-    dframes[((int64_t)b * frames + fr) * n + t] = out[f * n + t].x * w;
+    const float w = (wi >= 0 && wi < J.win) ? J.window[wi] : 0.f;
+    J.dframes[((int64_t)b * J.frames + fr) * n + t] = out[f * n + t].x * w;
   }
 }
 
@@ -168,13 +174,11 @@ __device__ __forceinline__ float padded_grad(const float* df, int i, int n, int 
   return s;
 }
 
-__global__ __launch_bounds__(256) void stft_bwd_fold_kernel(const float* __restrict__ dframes, int L,
-                                                            int n, int hop, int pad, int frames,
-                                                            float* __restrict__ gx) {
-  const int b = blockIdx.y;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void stft_bwd_fold_block(const StftJobD& J, int jblk, int b) {
+  const int j = jblk * blockDim.x + threadIdx.x;
+  const int L = J.L, n = J.n, hop = J.hop, pad = J.pad, frames = J.frames;
   if (j >= L) return;
-  const float* df = dframes + (int64_t)b * frames * n;
+  const float* df = J.dframes + (int64_t)b * frames * n;
   const int P = L + 2 * pad;
   float g = 0.f;
   // centre copy: padded index j + pad
@@ -186,7 +190,62 @@ __global__ __launch_bounds__(256) void stft_bwd_fold_kernel(const float* __restr
     const int i = 2 * (L - 1) - j + pad;
     if (i >= pad + L && i < P) g += padded_grad(df, i, n, hop, frames);
   }
-  gx[(int64_t)b * L + j] = g;
+  J.gx[(int64_t)b * L + j] = g;
+}
+
+// ---- launch-level: one job (grid.y = utterance) or up to MAX_JOBS jobs in
+// one launch (grid.x runs over every job's blocks; a block finds its job in
+// the prefix table), so the ten transforms of an MR-STFT loss fill the chip
+// as one launch instead of ten small ones
+constexpr int STFT_MAX_JOBS = 16;
+struct StftJobs {
+  StftJobD job[STFT_MAX_JOBS];
+  int end[STFT_MAX_JOBS];  // exclusive prefix of blocks per job
+  int per_b[STFT_MAX_JOBS];  // blocks per utterance
+  int njobs;
+};
+
+__device__ __forceinline__ int find_job(const StftJobs& J, int blk) {
+  int j = 0;
+  while (j + 1 < J.njobs && blk >= J.end[j]) ++j;
+  return j;
+}
+
+__global__ __launch_bounds__(256) void stft_fwd_kernel(const StftJobD J) {
+  extern __shared__ float2 sfft[];
+  stft_fwd_block(J, blockIdx.x, blockIdx.y, sfft);
+}
+
+__global__ __launch_bounds__(256) void stft_fwd_multi_kernel(const StftJobs J) {
+  extern __shared__ float2 sfft[];
+  const int j = find_job(J, blockIdx.x);
+  const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
+  const int b = local / J.per_b[j];
+  stft_fwd_block(J.job[j], local - b * J.per_b[j], b, sfft);
+}
+
+__global__ __launch_bounds__(256) void stft_bwd_frames_kernel(const StftJobD J) {
+  extern __shared__ float2 sfft[];
+  stft_bwd_frames_block(J, blockIdx.x, blockIdx.y, sfft);
+}
+
+__global__ __launch_bounds__(256) void stft_bwd_frames_multi_kernel(const StftJobs J) {
+  extern __shared__ float2 sfft[];
+  const int j = find_job(J, blockIdx.x);
+  const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
+  const int b = local / J.per_b[j];
+  stft_bwd_frames_block(J.job[j], local - b * J.per_b[j], b, sfft);
+}
+
+__global__ __launch_bounds__(256) void stft_bwd_fold_kernel(const StftJobD J) {
+  stft_bwd_fold_block(J, blockIdx.x, blockIdx.y);
+}
+
+__global__ __launch_bounds__(256) void stft_bwd_fold_multi_kernel(const StftJobs J) {
+  const int j = find_job(J, blockIdx.x);
+  const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
+  const int b = local / J.per_b[j];
+  stft_bwd_fold_block(J.job[j], local - b * J.per_b[j], b);
 }
 
 int ilog2(int n) {
@@ -194,6 +253,33 @@ int ilog2(int n) {
   while ((1 << l) < n) ++l;
   return (1 << l) == n ? l : -1;
 }
+
+// host: fill one device job from the C-ABI arguments; 0 or a VITS_E code
+int make_job(StftJobD& J, const float* x, int batch, int length, const float* window, int n_fft,
+             int hop, int win, int pad, float eps) {
+  VITS_CHECK_ARG(window && batch > 0 && length > 0 && hop > 0 && win > 0);
+  const int log2n = ilog2(n_fft);
+  VITS_CHECK_SHAPE(log2n >= 1 && n_fft <= FFT_MAX && win <= n_fft && pad >= 0 && pad < length);
+  const int frames = (length + 2 * pad - n_fft) / hop + 1;
+  VITS_CHECK_SHAPE(frames > 0);
+  J = StftJobD{};
+  J.x = x;
+  J.window = window;
+  J.L = length;
+  J.n = n_fft;
+  J.log2n = log2n;
+  J.hop = hop;
+  J.win = win;
+  J.pad = pad;
+  J.frames = frames;
+  J.fpb = n_fft >= 1024 ? 1 : 1024 / n_fft;
+  J.batch = batch;
+  J.eps = eps;
+  return VITS_OK;
+}
+
+size_t job_lds(const StftJobD& J) { return sizeof(float2) * (2 * J.fpb * J.n + J.n / 2); }
+int job_fblocks(const StftJobD& J) { return (J.frames + J.fpb - 1) / J.fpb; }
 
 }  // namespace
 
@@ -207,16 +293,15 @@ extern "C" int64_t vits_stft_workspace(int batch, int length, int n_fft, int hop
 extern "C" int vits_stft_mag_forward(const float* x, int batch, int length, const float* window,
                                      int n_fft, int hop, int win, int pad, float eps, float* mag,
                                      float* re, float* im, void* stream) {
-  VITS_CHECK_ARG(x && window && mag && batch > 0 && length > 0 && hop > 0 && win > 0);
-  const int log2n = ilog2(n_fft);
-  VITS_CHECK_SHAPE(log2n >= 1 && n_fft <= FFT_MAX && win <= n_fft && pad >= 0 && pad < length);
-  const int frames = (length + 2 * pad - n_fft) / hop + 1;
-  VITS_CHECK_SHAPE(frames > 0);
-  const int fpb = n_fft >= 1024 ? 1 : 1024 / n_fft;
-  const size_t lds = sizeof(float2) * (2 * fpb * n_fft + n_fft / 2);
-  dim3 grid((frames + fpb - 1) / fpb, batch);
-  hipLaunchKernelGGL(stft_fwd_kernel, grid, dim3(256), lds, as_stream(stream), x, length, window,
-                     n_fft, log2n, hop, win, pad, frames, fpb, eps, mag, re, im);
+  VITS_CHECK_ARG(x && mag);
+  StftJobD J;
+  int rc = make_job(J, x, batch, length, window, n_fft, hop, win, pad, eps);
+  if (rc) return rc;
+  J.mag = mag;
+  J.re = re;
+  J.im = im;
+  dim3 grid(job_fblocks(J), batch);
+  hipLaunchKernelGGL(stft_fwd_kernel, grid, dim3(256), job_lds(J), as_stream(stream), J);
   return vits_launch_status();
 }
 
@@ -224,23 +309,96 @@ extern "C" int vits_stft_mag_backward(const float* grad_mag, const float* mag, c
                                       const float* im, const float* window, int batch, int length,
                                       int n_fft, int hop, int win, int pad, float* grad_x,
                                       float* workspace, int64_t workspace_floats, void* stream) {
-  VITS_CHECK_ARG(grad_mag && mag && re && im && window && grad_x && workspace);
-  VITS_CHECK_ARG(batch > 0 && length > 0 && hop > 0 && win > 0);
-  const int log2n = ilog2(n_fft);
-  VITS_CHECK_SHAPE(log2n >= 1 && n_fft <= FFT_MAX && win <= n_fft && pad >= 0 && pad < length);
-  const int frames = (length + 2 * pad - n_fft) / hop + 1;
-  VITS_CHECK_SHAPE(frames > 0);
+  VITS_CHECK_ARG(grad_mag && mag && re && im && grad_x && workspace);
+  StftJobD J;
+  int rc = make_job(J, nullptr, batch, length, window, n_fft, hop, win, pad, 0.f);
+  if (rc) return rc;
   if (workspace_floats < vits_stft_workspace(batch, length, n_fft, hop, pad)) return VITS_E_ARG;
-  const int fpb = n_fft >= 1024 ? 1 : 1024 / n_fft;
-  const size_t lds = sizeof(float2) * (2 * fpb * n_fft + n_fft / 2);
+  J.gmag = grad_mag;
+  J.mag = const_cast<float*>(mag);
+  J.re = const_cast<float*>(re);
+  J.im = const_cast<float*>(im);
+  J.dframes = workspace;
+  J.gx = grad_x;
   hipStream_t s = as_stream(stream);
-  dim3 grid((frames + fpb - 1) / fpb, batch);
-  hipLaunchKernelGGL(stft_bwd_frames_kernel, grid, dim3(256), lds, s, grad_mag, mag, re, im,
-                     window, n_fft, log2n, win, frames, fpb, workspace);
+  hipLaunchKernelGGL(stft_bwd_frames_kernel, dim3(job_fblocks(J), batch), dim3(256), job_lds(J), s,
+                     J);
+  rc = vits_launch_status();
+  if (rc) return rc;
+  hipLaunchKernelGGL(stft_bwd_fold_kernel, dim3((length + 255) / 256, batch), dim3(256), 0, s, J);
+  return vits_launch_status();
+}
+
+extern "C" int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs, void* stream) {
+  VITS_CHECK_ARG(jobs && njobs > 0 && njobs <= STFT_MAX_JOBS);
+  StftJobs M{};
+  M.njobs = njobs;
+  size_t lds = 0;
+  int blocks = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const vits_stft_job& q = jobs[i];
+    VITS_CHECK_ARG(q.x && q.mag);
+    int rc = make_job(M.job[i], q.x, q.batch, q.length, q.window, q.n_fft, q.hop, q.win, q.pad,
+                      q.eps);
+    if (rc) return rc;
+    M.job[i].mag = q.mag;
+    M.job[i].re = q.re;
+    M.job[i].im = q.im;
+    M.per_b[i] = job_fblocks(M.job[i]);
+    blocks += M.per_b[i] * q.batch;
+    M.end[i] = blocks;
+    lds = job_lds(M.job[i]) > lds ? job_lds(M.job[i]) : lds;
+  }
+  hipLaunchKernelGGL(stft_fwd_multi_kernel, dim3(blocks), dim3(256), lds, as_stream(stream), M);
+  return vits_launch_status();
+}
+
+extern "C" int64_t vits_stft_workspace_multi(const vits_stft_job* jobs, int njobs) {
+  if (!jobs || njobs <= 0) return 0;
+  int64_t tot = 0;
+  for (int i = 0; i < njobs; ++i)
+    tot += vits_stft_workspace(jobs[i].batch, jobs[i].length, jobs[i].n_fft, jobs[i].hop,
+                               jobs[i].pad);
+  return tot;
+}
+
+extern "C" int vits_stft_mag_backward_multi(const vits_stft_job* jobs, int njobs,
+                                            float* workspace, int64_t workspace_floats,
+                                            void* stream) {
+  VITS_CHECK_ARG(jobs && njobs > 0 && njobs <= STFT_MAX_JOBS && workspace);
+  if (workspace_floats < vits_stft_workspace_multi(jobs, njobs)) return VITS_E_ARG;
+  StftJobs M{}, F{};
+  M.njobs = F.njobs = njobs;
+  size_t lds = 0;
+  int blocks = 0, fblocks = 0;
+  int64_t woff = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const vits_stft_job& q = jobs[i];
+    VITS_CHECK_ARG(q.grad_mag && q.mag && q.re && q.im && q.grad_x);
+    int rc = make_job(M.job[i], nullptr, q.batch, q.length, q.window, q.n_fft, q.hop, q.win,
+                      q.pad, 0.f);
+    if (rc) return rc;
+    StftJobD& J = M.job[i];
+    J.gmag = q.grad_mag;
+    J.mag = q.mag;
+    J.re = q.re;
+    J.im = q.im;
+    J.dframes = workspace + woff;
+    J.gx = q.grad_x;
+    woff += vits_stft_workspace(q.batch, q.length, q.n_fft, q.hop, q.pad);
+    F.job[i] = J;
+    M.per_b[i] = job_fblocks(J);
+    blocks += M.per_b[i] * q.batch;
+    M.end[i] = blocks;
+    F.per_b[i] = (q.length + 255) / 256;
+    fblocks += F.per_b[i] * q.batch;
+    F.end[i] = fblocks;
+    lds = job_lds(J) > lds ? job_lds(J) : lds;
+  }
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(stft_bwd_frames_multi_kernel, dim3(blocks), dim3(256), lds, s, M);
   int rc = vits_launch_status();
   if (rc) return rc;
-  dim3 g2((length + 255) / 256, batch);
-  hipLaunchKernelGGL(stft_bwd_fold_kernel, g2, dim3(256), 0, s, workspace, length, n_fft, hop, pad,
-                     frames, grad_x);
+  hipLaunchKernelGGL(stft_bwd_fold_multi_kernel, dim3(fblocks), dim3(256), 0, s, F);
   return vits_launch_status();
 }

@@ -620,6 +620,83 @@ class _StftMag(torch.autograd.Function):
         return gx, None, None, None, None, None, None
 
 
+class _StftMagMulti(torch.autograd.Function):
+    """Magnitudes of several (signal, resolution) jobs in one launch each way
+    (vits_stft_mag_{forward,backward}_multi); gradients flow to every input
+    signal that requires them."""
+
+    @staticmethod
+    def forward(ctx, specs, *xs):
+        # specs: tuple of (window, n_fft, hop, win, pad, eps) per job
+        require_device(*xs)
+        jobs = (_lib.StftJob * len(xs))()
+        keep, mags, saved = [], [], []
+        for i, (x, (window, n_fft, hop, win, pad, eps)) in enumerate(zip(xs, specs)):
+            x = x.contiguous().float()
+            window = window.contiguous().float()
+            B, L = x.shape
+            frames = (L + 2 * pad - n_fft) // hop + 1
+            mag = torch.empty(B, n_fft // 2 + 1, frames, device=x.device, dtype=torch.float32)
+            need = ctx.needs_input_grad[i + 1]
+            re = torch.empty_like(mag) if need else None
+            im = torch.empty_like(mag) if need else None
+            j = jobs[i]
+            j.x, j.window, j.mag, j.re, j.im = x.data_ptr(), window.data_ptr(), mag.data_ptr(), \
+                _ptr(re), _ptr(im)
+            j.batch, j.length, j.n_fft, j.hop, j.win, j.pad, j.eps = B, L, n_fft, hop, win, pad, eps
+            keep += [x, window]
+            mags.append(mag)
+            saved.append((mag, re, im, window, B, L, n_fft, hop, win, pad) if need else None)
+        check(_lib.load().vits_stft_mag_forward_multi(jobs, len(xs), _stream_ptr(xs[0].device)),
+              "vits_stft_mag_forward_multi")
+        ctx.saved = saved
+        ctx.dev = xs[0].device
+        # magnitudes of signals that need no gradient (the MR-STFT target y)
+        # stay plain tensors, as torch.stft of such a signal would be
+        nd = [m for m, sv in zip(mags, saved) if sv is None]
+        if nd:
+            ctx.mark_non_differentiable(*nd)
+        return tuple(mags)
+
+    @staticmethod
+    def backward(ctx, *gmags):
+        idx = [i for i, sv in enumerate(ctx.saved) if sv is not None]
+        grads = [None] * len(ctx.saved)
+        if not idx:
+            return (None,) + tuple(grads)
+        jobs = (_lib.StftJob * len(idx))()
+        keep = []
+        for q, i in enumerate(idx):
+            mag, re, im, window, B, L, n_fft, hop, win, pad = ctx.saved[i]
+            g = gmags[i]
+            g = torch.zeros_like(mag) if g is None else g.contiguous().float()
+            gx = torch.empty(B, L, device=ctx.dev, dtype=torch.float32)
+            j = jobs[q]
+            j.grad_mag, j.mag, j.re, j.im, j.window, j.grad_x = g.data_ptr(), mag.data_ptr(), \
+                re.data_ptr(), im.data_ptr(), window.data_ptr(), gx.data_ptr()
+            j.batch, j.length, j.n_fft, j.hop, j.win, j.pad = B, L, n_fft, hop, win, pad
+            keep.append(g)
+            grads[i] = gx
+        lib = _lib.load()
+        nws = int(lib.vits_stft_workspace_multi(jobs, len(idx)))
+        ws = torch.empty(max(nws, 1), device=ctx.dev, dtype=torch.float32)
+        check(lib.vits_stft_mag_backward_multi(jobs, len(idx), ws.data_ptr(), ws.numel(),
+                                               _stream_ptr(ctx.dev)), "vits_stft_mag_backward_multi")
+        return (None,) + tuple(grads)
+
+
+def stft_mag_multi(xs, specs):
+    """[sqrt(|STFT(x_i)|^2 + eps_i)] for jobs (x_i, window_i, n_fft_i, hop_i,
+    win_i, pad_i, eps_i) in one launch (at most 16 jobs); differentiable in
+    every x_i.  specs: sequence of (window, n_fft, hop, win, pad, eps)."""
+    if len(xs) > 16:
+        raise _lib.VitsAmdError("stft_mag_multi: at most 16 jobs per launch")
+    specs = tuple((w, int(n), int(h), int(wl), int(n) // 2 if p is None else int(p), float(e))
+                  for (w, n, h, wl, p, e) in specs)
+    # cast outside the Function so autograd returns gradients in each x's dtype
+    return list(_StftMagMulti.apply(specs, *[x.float() for x in xs]))
+
+
 def stft_mag(x: torch.Tensor, window: torch.Tensor, n_fft: int, hop: int, win: int,
              pad: Optional[int] = None, eps: float = 1e-7) -> torch.Tensor:
     """sqrt(|STFT(x)|^2 + eps), [B, n_fft//2+1, frames]; differentiable in x."""
