@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn import Conv1d, Conv2d, LeakyReLU
 from torch.nn.utils import spectral_norm, weight_norm
+from torch.nn.utils.spectral_norm import SpectralNorm
 
 LRELU_SLOPE = 0.2
 
@@ -109,6 +110,50 @@ class MultiSTFTDiscriminator(nn.Module):
         return [d(x) for x, d in zip(xs, self.discriminators)]
 
 
+class GroupedSpectralNorm:
+    """Spectral norm of every conv of a module tree, computed once per
+    forward and batched over layers of equal weight shape.
+
+    Same state (``weight_orig`` parameter, ``weight_u`` / ``weight_v``
+    buffers, so ``D_*.pth`` checkpoints load unchanged) and the same math as
+    ``torch.nn.utils.spectral_norm`` (one power iteration per forward in
+    training mode, u / v updated in place and cloned, sigma = u^T W v,
+    W / sigma): the per-layer forward pre-hooks (~10 small ops and ~0.2 ms
+    of host time each, 85 layers x 3 forwards per train_stft step) become
+    one batched power iteration per weight shape (bmm instead of mv)."""
+
+    def __init__(self, root: nn.Module):
+        self.root = root
+        self.groups = {}
+        for m in root.modules():
+            for k, hook in list(m._forward_pre_hooks.items()):
+                if isinstance(hook, SpectralNorm):
+                    if hook.dim != 0 or hook.n_power_iterations != 1:
+                        continue  # keep torch's hook for other settings
+                    del m._forward_pre_hooks[k]
+                    key = (tuple(getattr(m, hook.name + "_orig").shape), hook.eps, hook.name)
+                    self.groups.setdefault(key, []).append(m)
+
+    def apply(self, training: bool):
+        for (shape, eps, name), mods in self.groups.items():
+            W = torch.stack([getattr(m, name + "_orig") for m in mods])  # [G, out, ...]
+            G, h = W.shape[0], W.shape[1]
+            mat = W.reshape(G, h, -1)
+            u = torch.stack([getattr(m, name + "_u") for m in mods])
+            v = torch.stack([getattr(m, name + "_v") for m in mods])
+            if training:
+                with torch.no_grad():
+                    v = F.normalize(torch.bmm(mat.transpose(1, 2), u.unsqueeze(-1)).squeeze(-1),
+                                    dim=1, eps=eps)
+                    u = F.normalize(torch.bmm(mat, v.unsqueeze(-1)).squeeze(-1), dim=1, eps=eps)
+                    torch._foreach_copy_([getattr(m, name + "_u") for m in mods], list(u.unbind(0)))
+                    torch._foreach_copy_([getattr(m, name + "_v") for m in mods], list(v.unbind(0)))
+            sigma = (u * torch.bmm(mat, v.unsqueeze(-1)).squeeze(-1)).sum(-1)  # [G]
+            Wn = W / sigma.view(G, *([1] * (W.dim() - 1)))
+            for m, w in zip(mods, Wn.unbind(0)):
+                setattr(m, name, w)
+
+
 class MultiWaveSTFTDiscriminator(nn.Module):
     def __init__(self,
                  multi_wave_discriminator_params={"num_dwt": 5, "kernel_size": 5, "layers": 10,
@@ -123,8 +168,10 @@ class MultiWaveSTFTDiscriminator(nn.Module):
         super().__init__()
         self.mwd = MultiWaveDiscriminator(**multi_wave_discriminator_params)
         self.mfd = MultiSTFTDiscriminator(**multi_stft_discriminator_params)
+        self.__dict__["_sn"] = GroupedSpectralNorm(self)
 
     def forward(self, x, m):
         """x [B, 1, t] waveform, m list of STFT magnitudes [B, F, T] (the
         MR-STFT loss's outputs, train_stft.py:198-199)."""
+        self._sn.apply(self.training)
         return self.mwd(x) + self.mfd(m)
