@@ -268,6 +268,47 @@ int vits_attention_forward(const float* q, const float* k, const float* v, float
                            int64_t qkv_bstride, int64_t out_bstride, const int32_t* lengths,
                            void* stream);
 
+/* ---------------------------------------------------------------------- */
+/* Training-step convs (backward of every stride-1 nn.Conv1d the          */
+/* train_stft.py step runs under fp16 autocast, train_stft.py:165-236:    */
+/* WN modules.py:130-182, ResBlock2 modules.py:250-260, couplings         */
+/* modules.py:357-375, PosteriorEncoder models.py:268-279, Generator      */
+/* models.py:306-318, WaveDiscriminator mrd.py:15-55).  The forward and   */
+/* the input gradient run through vits_conv1d_forward on a 16-bit image   */
+/* of the weight; the weight gradient has its own kernel.                 */
+/* ---------------------------------------------------------------------- */
+/* fp32 W [cout][cin][k] -> 16-bit image [cin_pad/16][k][2][m_pad][8] of   */
+/* wdtype (VITS_WDT_F16 / _BF16).  transpose = 0: rows = co, channels =   */
+/* ci (forward).  transpose = 1: rows = ci, channels = co, taps reversed  */
+/* (input gradient: dX = conv(dY, W', pad_left = (k-1)*dil - pad)).       */
+int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, void* out,
+                       int m_pad, int cin_pad, int wdtype, void* stream);
+
+typedef struct vits_conv1d_wgrad_desc {
+  const float* dy;        /* output gradient [B][cout][n_out], t contiguous  */
+  int64_t dy_bstride;
+  int32_t dy_cstride;
+  int32_t cout;
+  const float* x;         /* forward input [B][cin][tin], t contiguous       */
+  int64_t x_bstride;
+  int32_t x_cstride;
+  int32_t cin;
+  int32_t tin;
+  int32_t n_out;
+  int32_t k;
+  int32_t dil;
+  int32_t pad_left;       /* forward: output t reads x[t - pad_left + j*dil] */
+  float in_slope;         /* forward's leaky-relu prologue slope (1 = none)  */
+  float* dw_t;            /* += dW as [k][cout][cin] fp32 (caller zeroes)    */
+  float* dbias;           /* += sum_{b,t} dY [cout] fp32, or NULL            */
+  int32_t wdtype;         /* MFMA operand type: VITS_WDT_F16 / VITS_WDT_BF16 */
+  int32_t reserved;
+} vits_conv1d_wgrad_desc;
+/* dW[co][ci][j] = sum_{b,t} dY[b][co][t] * act(x[b][ci][t - pad_left + j*dil]) */
+/* (operands rounded to wdtype, fp32 accumulation; VITS_E_UNSUP when       */
+/* 64 + (k-1)*dil > 128 or k not in {1,2,3,4,5,7,9,11})                  */
+int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, void* stream);
+
 /* library introspection */
 const char* vits_amd_version(void);
 int vits_amd_device_arch(char* buf, int len);

@@ -1,0 +1,151 @@
+"""Training-conv parity (vits_amd/train_ops.py): forward, input gradient,
+weight and bias gradient of the HIP path against torch autograd in fp32 on
+the SAME fp16-rounded operands (x, W, dY rounded to fp16 as the reference's
+autocast convs round them, train_stft.py:165).  With identical operands the
+only difference is fp32 summation order, so the tolerance is 2e-4 of each
+tensor's max magnitude (the bias-free check below uses the unrounded dY for
+dbias, which the kernel sums in fp32 before rounding)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from vits_amd import train_ops
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-4
+
+
+def _close(a, b, what, tol=TOL):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    scale = b.abs().max().item() + 1e-12
+    err = (a - b).abs().max().item()
+    assert err <= tol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _r16(t):
+    return t.half().float()
+
+
+CASES = [
+    # B, cin, cout, k, dil, pad, T, slope
+    (2, 256, 512, 5, 1, 2, 500, 1.0),      # WN in_layer (enc_q / flows)
+    (2, 256, 512, 1, 1, 0, 333, 1.0),      # WN res_skip
+    (3, 96, 256, 1, 1, 0, 130, 1.0),       # coupling pre
+    (2, 128, 128, 11, 5, 25, 768, 0.1),    # ResBlock2 c1 (leaky prologue, k11 d5)
+    (2, 32, 32, 7, 3, 9, 1500, 0.1),       # ResBlock2 c1, 32-channel stage
+    (2, 16, 32, 3, 1, 1, 1000, 1.0),       # ResBlock2 c2 (cin = C'/2)
+    (2, 192, 512, 7, 1, 3, 48, 1.0),       # conv_pre on a 48-frame slice
+    (2, 32, 1, 7, 1, 3, 9216, 0.01),       # conv_post
+    (2, 64, 64, 5, 9, 0, 700, 0.2),        # WaveDiscriminator dilated valid conv
+    (2, 1, 64, 1, 1, 0, 1000, 1.0),        # WaveDiscriminator input conv
+    (1, 513, 256, 1, 1, 0, 77, 1.0),       # PosteriorEncoder pre (ragged T)
+    (2, 160, 160, 5, 4, 0, 301, 0.2),      # MWD scale 3, odd length
+]
+
+
+@pytest.mark.parametrize("B,cin,cout,k,dil,pad,T,slope", CASES)
+def test_conv1d_train_fwd_bwd(device, B, cin, cout, k, dil, pad, T, slope):
+    g = torch.Generator().manual_seed(B * 7919 + cin * 31 + cout + k * 3 + dil)
+    x = torch.randn(B, cin, T, generator=g)
+    w = torch.randn(cout, cin, k, generator=g) / (cin * k) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    T_out = T + 2 * pad - (k - 1) * dil
+    dy = torch.randn(B, cout, T_out, generator=g)
+
+    xd = x.to(device).requires_grad_(True)
+    wd = w.to(device).requires_grad_(True)
+    bd = b.to(device).requires_grad_(True)
+    y = train_ops.Conv1dHip.apply(xd, wd, bd, dil, pad, slope, train_ops.TRAIN_WDTYPE)
+    y.backward(dy.to(device))
+
+    xr = _r16(x).requires_grad_(True)
+    wr = _r16(w).requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    xa = F.leaky_relu(xr, slope) if slope != 1.0 else xr
+    # the kernel rounds the ACTIVATED input: round after the prologue
+    xa16 = xa + (_r16(xa.detach()) - xa.detach())
+    yr = F.conv1d(xa16, wr, br, padding=pad, dilation=dil)
+    yr.backward(_r16(dy))
+    _close(y, yr, "y")
+    _close(xd.grad, xr.grad, "dx")
+    _close(wd.grad, wr.grad, "dw")
+    # dbias: the kernel sums the unrounded fp32 dY
+    _close(bd.grad, dy.sum((0, 2)), "db")
+
+
+def test_conv1d_train_module_helper_matches_torch_module(device):
+    """train_ops.conv1d on a weight-normed module: same forward and the
+    gradients reach weight_g / weight_v through torch._weight_norm."""
+    torch.manual_seed(0)
+    conv = torch.nn.utils.weight_norm(torch.nn.Conv1d(64, 128, 5, padding=4, dilation=2))
+    ref = torch.nn.utils.weight_norm(torch.nn.Conv1d(64, 128, 5, padding=4, dilation=2))
+    ref.load_state_dict(conv.state_dict())
+    conv = conv.to(device)
+    x = torch.randn(2, 64, 300)
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = train_ops.conv1d(conv, x.to(device), in_slope=0.1)
+    assert y.dtype == torch.float32  # the HIP op (a torch autocast conv returns fp16)
+    y.square().sum().backward()
+    yr = ref(F.leaky_relu(x, 0.1))
+    yr.square().sum().backward()
+    _close(y, yr, "y", tol=3e-3)   # fp16 operands vs fp32 torch
+    for name in ("weight_g", "weight_v", "bias"):
+        _close(getattr(conv, name).grad, getattr(ref, name).grad, name, tol=5e-3)
+
+
+def test_conv1d_train_autocast(device):
+    """Under fp16 autocast the op takes fp16 inputs, returns fp32 and its
+    gradients flow back to the fp16 producer."""
+    conv = torch.nn.Conv1d(32, 32, 3, padding=1).to(device)
+    x = torch.randn(2, 32, 100, device=device, requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.float16):
+        h = x * 2.0
+        h16 = h.half()
+        y = train_ops.conv1d(conv, h16)
+    assert y.dtype == torch.float32
+    y.sum().backward()
+    assert x.grad is not None and torch.isfinite(x.grad).all()
+    assert conv.weight.grad is not None and conv.bias.grad is not None
+
+
+def test_conv1d_train_fp32_mode_is_torch(device):
+    """Without autocast the reference trains in fp32; the helper keeps torch's
+    fp32 conv there (bit-identical to calling the module)."""
+    conv = torch.nn.Conv1d(16, 16, 3, padding=1).to(device)
+    x = torch.randn(1, 16, 50, device=device)
+    assert torch.equal(train_ops.conv1d(conv, x, in_slope=0.2), conv(F.leaky_relu(x, 0.2)))
+
+
+def test_training_forward_autocast_hip_convs(device):
+    """Tiny-config training forward under fp16 autocast (HIP convs with fp16
+    operands) against the same forward with torch autocast convs: the two
+    round operands identically, so the waveform slices agree to ~1e-3."""
+    from common import build_model, golden, tiny_cfg
+    from vits_amd import train_ops as T
+
+    c = tiny_cfg()
+    m = build_model(c["model"], c["data"], device)
+    gd = golden("tiny_forward.npz")
+    t = {k: torch.from_numpy(v) for k, v in gd.items()}
+    args = (t["x"].to(device), t["x_lengths"].to(device), t["spec"].to(device),
+            t["y_lengths"].to(device), t["emo"].to(device), t["sid"].to(device))
+    kw = dict(noise_q=t["noise_q"].to(device), noise_align=t["noise_align"].to(device),
+              noise_flow=t["noise_flow"].to(device))
+    outs = []
+    for use_hip in (True, False):
+        orig_rand, orig_wdt = torch.rand, T.autocast_wdtype
+        torch.rand = lambda *a, **k: t["rand_slice"].clone()
+        if not use_hip:
+            T.autocast_wdtype = lambda *a, **k: None
+        try:
+            with torch.autocast("cuda", dtype=torch.float16):
+                outs.append(m(*args, **kw))
+        finally:
+            torch.rand, T.autocast_wdtype = orig_rand, orig_wdt
+    (o_h, _, attn_h, ids_h), (o_t, _, attn_t, ids_t) = outs[0][:4], outs[1][:4]
+    assert torch.equal(ids_h, ids_t)
+    _close(o_h, o_t, "o", tol=2e-2)
+    _close(o_h, torch.from_numpy(gd["o"]), "o vs fp32 reference", tol=3e-2)

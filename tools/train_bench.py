@@ -23,8 +23,11 @@ def main():
     ap.add_argument("--no-mels", action="store_true")
     ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--torch-prof", default=None, help="write a torch.profiler op table here")
+    ap.add_argument("--cudnn-benchmark", action="store_true",
+                    help="torch.backends.cudnn.benchmark = True (train_stft.py:26)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    torch.backends.cudnn.benchmark = args.cudnn_benchmark
     hps = default_hps()
     torch.manual_seed(1234)
     g, d = build_models(hps, dev)

@@ -96,6 +96,29 @@ class StftJob(C.Structure):
     ]
 
 
+class ConvWgradDesc(C.Structure):
+    _fields_ = [
+        ("dy", C.c_void_p),
+        ("dy_bstride", C.c_int64),
+        ("dy_cstride", C.c_int32),
+        ("cout", C.c_int32),
+        ("x", C.c_void_p),
+        ("x_bstride", C.c_int64),
+        ("x_cstride", C.c_int32),
+        ("cin", C.c_int32),
+        ("tin", C.c_int32),
+        ("n_out", C.c_int32),
+        ("k", C.c_int32),
+        ("dil", C.c_int32),
+        ("pad_left", C.c_int32),
+        ("in_slope", C.c_float),
+        ("dw_t", C.c_void_p),
+        ("dbias", C.c_void_p),
+        ("wdtype", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
 _SIGS = {
     "vits_conv1d_forward": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_void_p]),
     "vits_conv1d_forward_seq": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_int, C.c_void_p]),
@@ -155,6 +178,11 @@ _SIGS = {
         C.c_int,
         [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p],
     ),
+    "vits_conv1d_pack16": (
+        C.c_int,
+        [C.c_void_p] + [C.c_int] * 4 + [C.c_void_p] + [C.c_int] * 3 + [C.c_void_p],
+    ),
+    "vits_conv1d_wgrad": (C.c_int, [C.POINTER(ConvWgradDesc), C.c_int, C.c_void_p]),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
 }

@@ -1,0 +1,330 @@
+// conv1d_train.hip — the backward side of the MFMA conv for the training
+// step (train_stft.py:162-236 through SynthesizerTrn.forward and the MWSD
+// discriminator): every stride-1 Conv1d of WN / ResBlock2 / couplings /
+// posterior encoder / Generator / WaveDiscriminator runs its forward, input
+// gradient and weight gradient on 16-bit MFMA with fp32 accumulation (the
+// reference runs these convs under fp16 autocast, train_stft.py:165,216).
+//
+//  * vits_conv1d_pack16: the layer's fp32 weight [Cout][Cin][k] (weight-norm
+//    / spectral-norm already applied by the caller) -> the 16-bit image the
+//    forward kernel streams ([cin_pad/16][k][2][m_pad][8], conv1d_impl.h),
+//    either as is (forward) or transposed and tap-flipped (input gradient:
+//    dX = conv(dY, W'[ci][co][k-1-j], pad' = (k-1)*dil - pad), which the
+//    forward kernel then runs unchanged).
+//  * vits_conv1d_wgrad: dW[co][ci][j] = sum_{b,t} dY[b][co][t] * X~[b][ci][t - pad + j*dil]
+//    (X~ = leaky-relu prologue of X when the forward fused one) and
+//    dbias[co] = sum_{b,t} dY[b][co][t].  GEMM rows = co, columns = ci (one
+//    accumulator set per tap), reduction over (b, t).
+//
+// wgrad structure: workgroup = 4 waves = 64 co x 64 ci x all k taps; each
+// wave owns a 32 co x 32 ci block of every tap (k accumulators).  Per chunk
+// of KT = 64 time steps the workgroup stages
+//    dY[64 co][64 t]              f16, row-major (t contiguous)  -> A operand
+//    X~[64 + (k-1)*dil t][64 ci]  f16, time-major (ci contiguous) -> B operand
+// into LDS (double-buffered, next chunk's global loads in flight under the
+// current chunk's MFMAs).  The A fragment (8 consecutive t of one co row) is
+// one ds_read_b128; the B fragment of tap j (8 consecutive t of one ci,
+// starting at any row t + j*dil) is two ds_read_b64_tr_b16 transposed
+// reads, so every tap reuses the one staged window at an arbitrary row
+// offset — no im2col, no per-tap copies.  The reduction over (b, t) is
+// split across workgroups (>= 16 chunks each, so the fp32 atomics that
+// combine them stay far below the chip's atomic byte rate); partial tiles
+// are added with global_atomic_add_f32 into a [k][Cout][Cin] accumulator
+// (two 128-byte row segments per wave instruction).
+#include "common.h"
+
+namespace {
+
+typedef short s16x4 __attribute__((__vector_size__(4 * sizeof(short))));
+typedef __attribute__((address_space(3))) s16x4* lds_s16x4_ptr;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int WG_M = 64;               // co rows per workgroup
+constexpr int WG_N = 64;               // ci columns per workgroup
+constexpr int KT = 64;                 // time steps per chunk
+constexpr int DY_LD = KT + 8;          // halves per staged dY row (144 B)
+constexpr int X_LD = WG_N + 4;         // halves per staged X row (136 B, 8-B aligned)
+constexpr int MAX_WR = 128;            // staged window rows: KT + (k-1)*dil <= MAX_WR
+constexpr int DY_HALVES = WG_M * DY_LD;
+constexpr int X_HALVES = MAX_WR * X_LD;
+constexpr int STAGE_HALVES = DY_HALVES + X_HALVES;
+
+template <int WT>
+struct Op16 {
+  typedef _Float16 T;
+  typedef f16x8 V8;
+};
+template <>
+struct Op16<VITS_WDT_BF16> {
+  typedef __bf16 T;
+  typedef bf16x8 V8;
+};
+
+template <int WT>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef typename Op16<WT>::T T;
+  T ha = (T)a, hb = (T)b;
+  uint16_t ua, ub;
+  __builtin_memcpy(&ua, &ha, 2);
+  __builtin_memcpy(&ub, &hb, 2);
+  return (uint32_t)ua | ((uint32_t)ub << 16);
+}
+
+template <int NK, int WT>
+__global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_conv1d_wgrad_desc p,
+                                                                     int tchunks, int total_chunks,
+                                                                     int chunks_per_wg) {
+  typedef typename Op16<WT>::V8 V8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int l32 = lane & 31;
+  const int lhi = lane >> 5;
+  const int wm = (wid >> 1) * 32;  // wave's co offset in the tile
+  const int wn = (wid & 1) * 32;   // wave's ci offset in the tile
+  const int m0 = blockIdx.z * WG_M;
+  const int c0 = blockIdx.y * WG_N;
+  const int ch_begin = blockIdx.x * chunks_per_wg;
+  const int ch_end = min(total_chunks, ch_begin + chunks_per_wg);
+  const int dil = p.dil;
+  const int wr = KT + (NK - 1) * dil;  // staged window rows
+  const float slope = p.in_slope;
+  const bool act_in = slope != 1.0f;
+  const bool do_bias = p.dbias != nullptr && blockIdx.y == 0;
+
+  f32x16 acc[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  float bsum[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bsum[q] = 0.f;
+
+  // ---- staging maps (fixed per thread) ------------------------------------
+  // dY: pair e = tid + 256 q -> row (e >> 5), columns 2 (e & 31) + {0, 1}
+  const int dy_row0 = tid >> 5;   // + 8 q
+  const int dy_col = 2 * (tid & 31);
+  // X: wave w stages channel pairs (2 (w + 4 i), +1), i < 8, window rows
+  // lane + 64 h, h < 2: every global load instruction reads 64 consecutive
+  // time steps of one channel row (256 B).
+  float dyv[16];
+  float xv[32];
+
+  auto gload = [&](int chunk) {
+    const int b = chunk / tchunks;
+    const int t0 = (chunk - b * tchunks) * KT;
+    const float* dyb = p.dy + (int64_t)b * p.dy_bstride;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int co = m0 + dy_row0 + 8 * q;
+      const int t = t0 + dy_col;
+      const float* src = dyb + (int64_t)co * p.dy_cstride + t;
+      const bool rok = co < p.cout;
+      dyv[2 * q] = (rok && t < p.n_out) ? src[0] : 0.f;
+      dyv[2 * q + 1] = (rok && t + 1 < p.n_out) ? src[1] : 0.f;
+    }
+    const float* xb = p.x + (int64_t)b * p.x_bstride;
+    const int ts = t0 - p.pad_left;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ci = c0 + 2 * (wid + 4 * i);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = lane + 64 * h;
+        const int t = ts + r;
+        const bool tok = r < wr && t >= 0 && t < p.tin;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const bool ok = tok && ci + e < p.cin;
+          xv[(i * 2 + h) * 2 + e] = ok ? xb[(int64_t)(ci + e) * p.x_cstride + t] : 0.f;
+        }
+      }
+    }
+  };
+  auto lstore = [&](uint16_t* st) {
+    uint32_t* dyl = reinterpret_cast<uint32_t*>(st);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float a = dyv[2 * q], bv = dyv[2 * q + 1];
+      if (do_bias) bsum[q] += a + bv;
+      dyl[((dy_row0 + 8 * q) * DY_LD + dy_col) >> 1] = pack2<WT>(a, bv);
+    }
+    uint32_t* xl = reinterpret_cast<uint32_t*>(st + DY_HALVES);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int cl = 2 * (wid + 4 * i);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = lane + 64 * h;
+        float v0 = xv[(i * 2 + h) * 2], v1 = xv[(i * 2 + h) * 2 + 1];
+        if (act_in) {
+          v0 = v0 < 0.f ? v0 * slope : v0;
+          v1 = v1 < 0.f ? v1 * slope : v1;
+        }
+        if (h == 0 || r < wr) xl[(r * X_LD + cl) >> 1] = pack2<WT>(v0, v1);
+      }
+    }
+  };
+
+  // ---- fragment addressing --------------------------------------------------
+  // A (dY rows): lane -> co row wm + l32, t = 16 s + 8 lhi .. + 7
+  // B (tap j): 16-lane group g = lane >> 4 reads ci columns wn + 16 (g & 1) + 4 pp
+  //   (pp = lane & 3) of rows 16 s + 8 (g >> 1) + qq (+4) + j dil (qq = (lane >> 2) & 3)
+  const int g = lane >> 4;
+  const int qq = (lane >> 2) & 3;
+  const int pp = lane & 3;
+  const int a_off = (wm + l32) * DY_LD + 8 * lhi;
+  const int b_off = DY_HALVES + (8 * (g >> 1) + qq) * X_LD + wn + 16 * (g & 1) + 4 * pp;
+
+  if (ch_begin < ch_end) {
+    gload(ch_begin);
+    lstore(lds);
+  }
+  __syncthreads();
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
+    const int it = ch - ch_begin;
+    uint16_t* cur = lds + (it & 1) * STAGE_HALVES;
+    uint16_t* nxt = lds + ((it + 1) & 1) * STAGE_HALVES;
+    const bool more = ch + 1 < ch_end;
+    if (more) gload(ch + 1);
+#pragma unroll
+    for (int s = 0; s < KT / 16; ++s) {
+      const V8 a = *reinterpret_cast<const V8*>(cur + a_off + 16 * s);
+#pragma unroll
+      for (int j = 0; j < NK; ++j) {
+        const uint16_t* bp = cur + b_off + (16 * s + j * dil) * X_LD;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(bp));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(bp + 4 * X_LD));
+        const s16x4 both[2] = {lo, hi};
+        V8 bb;
+        __builtin_memcpy(&bb, both, 16);
+        if constexpr (WT == VITS_WDT_F16)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bb, acc[j], 0, 0, 0);
+        else
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc[j], 0, 0, 0);
+      }
+    }
+    if (more) lstore(nxt);
+    __syncthreads();
+  }
+
+  // ---- epilogue: fp32 atomics into dw_t[j][co][ci] ---------------------------
+  const int ci = c0 + wn + l32;
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = m0 + wm + 8 * (r >> 2) + 4 * lhi + (r & 3);
+      if (co < p.cout && ci < p.cin)
+        unsafeAtomicAdd(p.dw_t + ((int64_t)j * p.cout + co) * p.cin + ci, acc[j][r]);
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float v = bsum[q];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+      const int co = m0 + dy_row0 + 8 * q;
+      if ((tid & 31) == 0 && co < p.cout) unsafeAtomicAdd(p.dbias + co, v);
+    }
+  }
+}
+
+template <int WT>
+int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s) {
+  const int tchunks = (d.n_out + KT - 1) / KT;
+  const int total = batch * tchunks;
+  const int tiles = ((d.cout + WG_M - 1) / WG_M) * ((d.cin + WG_N - 1) / WG_N);
+  // >= 16 chunks (1024 time steps) per workgroup: 512 FLOP per atomic byte;
+  // beyond that, about 1024 workgroups
+  int cpw = (int)(((int64_t)total * tiles + 1023) / 1024);
+  const int min_cpw = total < 16 ? total : 16;
+  if (cpw < min_cpw) cpw = min_cpw;
+  const int splits = (total + cpw - 1) / cpw;
+  dim3 grid(splits, (d.cin + WG_N - 1) / WG_N, (d.cout + WG_M - 1) / WG_M);
+  const size_t lds = 2 * STAGE_HALVES * sizeof(uint16_t);
+  switch (d.k) {
+#define VITS_WG_CASE(NK) \
+  case NK:               \
+    hipLaunchKernelGGL((wgrad_kernel<NK, WT>), grid, dim3(256), lds, s, d, tchunks, total, cpw); \
+    break;
+    VITS_WG_CASE(1)
+    VITS_WG_CASE(2)
+    VITS_WG_CASE(3)
+    VITS_WG_CASE(4)
+    VITS_WG_CASE(5)
+    VITS_WG_CASE(7)
+    VITS_WG_CASE(9)
+    VITS_WG_CASE(11)
+#undef VITS_WG_CASE
+    default:
+      return VITS_E_UNSUP;
+  }
+  return vits_launch_status();
+}
+
+// ---- weight image for the 16-bit forward kernel ------------------------------
+template <typename T>
+__global__ void pack16_kernel(const float* __restrict__ w, int cout, int cin, int k, int transpose,
+                              T* __restrict__ out, int m_pad, int cin_pad) {
+  // out[c/16][j][(c%16)/8][m][c%8]; rows m / channels c are (co, ci) or,
+  // transposed, (ci, co) with the tap order reversed
+  const int64_t total = (int64_t)cin_pad * k * m_pad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i & 7);
+    int64_t r = i >> 3;
+    const int m = (int)(r % m_pad);
+    r /= m_pad;
+    const int half = (int)(r & 1);
+    r >>= 1;
+    const int j = (int)(r % k);
+    const int cg = (int)(r / k);
+    const int c = cg * 16 + half * 8 + c8;
+    float v = 0.f;
+    if (!transpose) {
+      if (m < cout && c < cin) v = w[((int64_t)m * cin + c) * k + j];
+    } else {
+      if (m < cin && c < cout) v = w[((int64_t)c * cin + m) * k + (k - 1 - j)];
+    }
+    out[i] = (T)v;
+  }
+}
+
+}  // namespace
+
+extern "C" int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, void* stream) {
+  if (!d) return VITS_E_ARG;
+  VITS_CHECK_ARG(d->dy && d->x && d->dw_t);
+  VITS_CHECK_ARG(batch > 0 && d->cout > 0 && d->cin > 0 && d->k > 0 && d->dil > 0);
+  VITS_CHECK_SHAPE(d->n_out > 0 && d->tin > 0);
+  if (KT + (d->k - 1) * d->dil > MAX_WR) return VITS_E_UNSUP;
+  if (d->wdtype == VITS_WDT_F16) return wgrad_dispatch<VITS_WDT_F16>(*d, batch, as_stream(stream));
+  if (d->wdtype == VITS_WDT_BF16) return wgrad_dispatch<VITS_WDT_BF16>(*d, batch, as_stream(stream));
+  return VITS_E_ARG;
+}
+
+extern "C" int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, void* out,
+                                  int m_pad, int cin_pad, int wdtype, void* stream) {
+  VITS_CHECK_ARG(w && out && cout > 0 && cin > 0 && k > 0);
+  const int rows = transpose ? cin : cout;
+  const int chans = transpose ? cout : cin;
+  VITS_CHECK_SHAPE(m_pad % 128 == 0 && m_pad >= rows && cin_pad % 16 == 0 && cin_pad >= chans);
+  const int64_t total = (int64_t)cin_pad * k * m_pad;
+  const int64_t nblk = (total + 255) / 256;
+  const int blocks = (int)(nblk < 4096 ? nblk : 4096);
+  hipStream_t s = as_stream(stream);
+  if (wdtype == VITS_WDT_F16)
+    hipLaunchKernelGGL(pack16_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, w, cout, cin, k,
+                       transpose, reinterpret_cast<_Float16*>(out), m_pad, cin_pad);
+  else if (wdtype == VITS_WDT_BF16)
+    hipLaunchKernelGGL(pack16_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, w, cout, cin, k,
+                       transpose, reinterpret_cast<__bf16*>(out), m_pad, cin_pad);
+  else
+    return VITS_E_ARG;
+  return vits_launch_status();
+}

@@ -17,6 +17,8 @@ from torch.nn import Conv1d, Conv2d, LeakyReLU
 from torch.nn.utils import spectral_norm, weight_norm
 from torch.nn.utils.spectral_norm import SpectralNorm
 
+from . import train_ops
+
 LRELU_SLOPE = 0.2
 
 
@@ -43,7 +45,16 @@ class WaveDiscriminator(nn.Module):
         _xavier_reset(self)
 
     def forward(self, x):
-        return self.convs(x).squeeze(1)
+        # each LeakyReLU is fused into the next conv as its input prologue
+        # (train_ops.conv1d), so the activated tensor is never materialised
+        slope = 1.0
+        for layer in self.convs:
+            if isinstance(layer, LeakyReLU):
+                slope = layer.negative_slope
+            else:
+                x = train_ops.conv1d(layer, x, in_slope=slope)
+                slope = 1.0
+        return x.squeeze(1)
 
 
 class MultiWaveDiscriminator(nn.Module):

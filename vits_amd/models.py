@@ -23,7 +23,7 @@ from torch.nn import Conv1d, ConvTranspose1d
 from torch.nn import functional as F
 from torch.nn.utils import remove_weight_norm, weight_norm
 
-from . import attentions, commons, engine, modules
+from . import attentions, commons, engine, modules, train_ops
 from .commons import gen_sin_table, get_padding, init_weights
 from .monotonic_align import maximum_path
 from .ops import neg_cent as neg_cent_scores
@@ -198,9 +198,9 @@ class PosteriorEncoder(nn.Module):
 
     def forward(self, x, x_lengths, g=None, noise=None):
         x_mask = torch.unsqueeze(commons.sequence_mask(x_lengths, x.size(2)), 1).to(x.dtype)
-        x = self.pre(x) * x_mask
+        x = self.pre[1](train_ops.conv1d(self.pre[0], x)) * x_mask
         x = self.enc(x, x_mask, g=g)
-        stats = self.proj(x) * x_mask
+        stats = train_ops.conv1d(self.proj, x) * x_mask
         m, logs = torch.split(stats, self.out_channels, dim=1)
         if noise is None:
             noise = torch.randn_like(m)
@@ -244,14 +244,14 @@ class Generator(nn.Module):
         if not _needs_grad(self, x, g):
             # inference: HIP plan only (raises off-GPU; there is no CPU path)
             return engine.generator_forward(self, x, g)
-        x = self.conv_pre(x)
+        x = train_ops.conv1d(self.conv_pre, x)
         for i in range(self.num_upsamples):
             x = self.ups[i](F.leaky_relu(x, modules.LRELU_SLOPE))
             xs = 0
             for j in range(self.num_kernels):
                 xs = xs + self.resblocks[i * self.num_kernels + j](x, g=g)
             x = xs / self.num_kernels
-        x = self.conv_post(F.leaky_relu(x))
+        x = train_ops.conv1d(self.conv_post, x, in_slope=0.01)  # F.leaky_relu default slope
         return torch.tanh(x)
 
     def infer(self, x, g):

@@ -17,6 +17,7 @@ from torch import nn
 from torch.nn import functional as F
 from torch.nn.utils import weight_norm, remove_weight_norm  # noqa: F401  (legacy names)
 
+from . import train_ops
 from .commons import get_padding, init_weights
 
 LRELU_SLOPE = 0.1
@@ -76,8 +77,9 @@ class WN(nn.Module):
         if self.gin_channels != 0:
             g = self.cond_layer(g)
         for i in range(self.n_layers):
-            acts = self.drop(self._gate(self.in_layers[i](x), g if self.gin_channels else None, i))
-            rs = self.res_skip_layers[i](acts)
+            x_in = train_ops.conv1d(self.in_layers[i], x)
+            acts = self.drop(self._gate(x_in, g if self.gin_channels else None, i))
+            rs = train_ops.conv1d(self.res_skip_layers[i], acts)
             if i < self.n_layers - 1:
                 x = (x + rs[:, :H]) * x_mask
                 output = output + rs[:, H:]
@@ -116,11 +118,11 @@ class ResBlock2(nn.Module):
 
             return resblock_infer(self, x, g)
         for c1, c2, cs in zip(self.convs1, self.convs2, self.conds):
-            xt = c1(F.leaky_relu(x, LRELU_SLOPE))
+            xt = train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE)
             xa, xb = torch.chunk(xt, 2, dim=1)
             sa, sb = torch.chunk(cs(g), 2, dim=1)
             xt = torch.tanh(xa + sa.unsqueeze(-1)) * torch.sigmoid(xb + sb.unsqueeze(-1))
-            x = c2(xt) + x
+            x = train_ops.conv1d(c2, xt) + x
         return x
 
     def infer(self, x, g=None):
@@ -162,9 +164,9 @@ class ResidualCouplingLayer(nn.Module):
         self.post.bias.data.zero_()
 
     def _stats(self, x0, x_mask, g):
-        h = self.pre(x0) * x_mask
+        h = train_ops.conv1d(self.pre, x0) * x_mask
         h = self.enc(h, x_mask, g=g)
-        stats = self.post(h) * x_mask
+        stats = train_ops.conv1d(self.post, h) * x_mask
         if not self.mean_only:
             m, logs = torch.split(stats, [self.half_channels] * 2, 1)
         else:

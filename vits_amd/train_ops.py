@@ -1,0 +1,162 @@
+"""Training-step convs on the HIP kernels (forward, input gradient, weight
+gradient), as autograd functions.
+
+The train_stft.py step (train_stft.py:162-236) runs every nn.Conv1d of the
+generator (WN modules.py:130-182, ResBlock2 modules.py:250-260, couplings
+modules.py:357-375, PosteriorEncoder models.py:268-279, Generator
+models.py:306-318) and of the MWSD wave discriminators (mrd.py:15-55) under
+fp16 autocast.  Here each such conv is one ``Conv1dHip`` call:
+
+* forward: ``vits_conv1d_forward`` on a 16-bit image of the fp32 weight
+  (``vits_conv1d_pack16``), activations fp32 in HBM, rounded to fp16 when
+  staged, fp32 accumulation; an optional leaky-relu on the input (the
+  ``F.leaky_relu`` / ``nn.LeakyReLU`` that precedes the conv in the
+  reference) is fused into the staging, so the activated tensor is never
+  materialised;
+* input gradient: the same forward kernel on the transposed, tap-reversed
+  weight image (dX = conv(dY, W'), pad' = (k-1)*dil - pad), times the
+  leaky-relu derivative of the saved input;
+* weight / bias gradient: ``vits_conv1d_wgrad`` (MFMA over the (b, t)
+  reduction, bias sum fused).
+
+Autocast: inputs are cast to fp32 and autocast is disabled inside
+(``custom_fwd(cast_inputs=float32)``); outputs are fp32.  The reference's
+autocast convs round inputs/weights to fp16 and return fp16; here operands
+are rounded the same way but results stay fp32 (GradScaler overflow
+semantics are the same: an fp16-overflowing gradient becomes inf).
+
+``conv1d`` selects the path: inside a 16-bit autocast region on a ROCm
+device (the reference's ``fp16_run``) it is always the HIP path and raises if
+the library is missing; in fp32 training (autocast off) and on CPU it is the
+torch conv, i.e. the reference's own fp32 arithmetic.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib
+from ._lib import EPI_STORE, WDT_BF16, WDT_F16, ConvWgradDesc, check
+from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, conv1d_launch, make_desc, make_out,
+                  weight_norm_effective)
+
+_TORCH_16 = {WDT_F16: torch.float16, WDT_BF16: torch.bfloat16}
+TRAIN_WDTYPE = WDT_F16  # the reference's autocast dtype (train_stft.py:165)
+
+
+def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype: int,
+            bias: torch.Tensor | None = None) -> PackedConv:
+    cout, cin, k = w32.shape
+    rows, chans = (cin, cout) if transpose else (cout, cin)
+    m_pad = (rows + 127) // 128 * 128
+    cin_pad = (chans + 15) // 16 * 16
+    img = torch.empty(cin_pad // 16, k, 2, m_pad, 8, dtype=_TORCH_16[wdtype], device=w32.device)
+    check(_lib.load().vits_conv1d_pack16(w32.data_ptr(), cout, cin, k, int(transpose),
+                                         img.data_ptr(), m_pad, cin_pad, wdtype,
+                                         _stream_ptr(w32.device)), "vits_conv1d_pack16")
+    return PackedConv(img, bias, chans, rows, k, dil, pad_left, EPI_STORE,
+                      _pick_tile_bf16(rows, k), 16, out_channels=rows, wdtype=wdtype)
+
+
+def _run(x: torch.Tensor, layer: PackedConv, n_out: int, in_slope: float = 1.0) -> torch.Tensor:
+    B = x.shape[0]
+    y = torch.empty(B, layer.m, n_out, device=x.device, dtype=torch.float32)
+    d = make_desc(layer, x, make_out(y), in_slope=in_slope, tin=x.shape[2], n_out=n_out)
+    conv1d_launch(d, B, x.device)
+    return y
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, k: int, dil: int, pad_left: int,
+          in_slope: float = 1.0, with_bias: bool = True, wdtype: int = TRAIN_WDTYPE):
+    """dW [Cout, Cin, k] and dbias [Cout] (fp32) of y = conv1d(act(x), W) + b."""
+    B, cout, n_out = dy.shape
+    _, cin, tin = x.shape
+    assert dy.stride(2) == 1 and x.stride(2) == 1 and dy.dtype == x.dtype == torch.float32
+    dw_t = torch.zeros(k, cout, cin, device=dy.device, dtype=torch.float32)
+    db = torch.zeros(cout, device=dy.device, dtype=torch.float32) if with_bias else None
+    d = ConvWgradDesc()
+    d.dy, d.dy_bstride, d.dy_cstride, d.cout = dy.data_ptr(), dy.stride(0), dy.stride(1), cout
+    d.x, d.x_bstride, d.x_cstride, d.cin = x.data_ptr(), x.stride(0), x.stride(1), cin
+    d.tin, d.n_out, d.k, d.dil, d.pad_left = tin, n_out, k, dil, pad_left
+    d.in_slope = in_slope
+    d.dw_t = dw_t.data_ptr()
+    d.dbias = None if db is None else db.data_ptr()
+    d.wdtype = wdtype
+    check(_lib.load().vits_conv1d_wgrad(d, B, _stream_ptr(dy.device)), "vits_conv1d_wgrad")
+    return dw_t.permute(1, 2, 0).contiguous(), db
+
+
+class Conv1dHip(torch.autograd.Function):
+    """y = conv1d(leaky_relu(x, in_slope), weight, bias, dilation, padding),
+    stride 1, zero padding, fp32 in/out, 16-bit MFMA operands."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x, weight, bias, dilation: int, padding: int, in_slope: float, wdtype: int):
+        x = x.contiguous()
+        w32 = weight.detach().contiguous()
+        k = w32.shape[2]
+        n_out = x.shape[2] + 2 * padding - (k - 1) * dilation
+        b32 = None if bias is None else bias.detach().contiguous()
+        layer = _pack16(w32, False, dilation, padding, wdtype, b32)
+        y = _run(x, layer, n_out, in_slope)
+        ctx.save_for_backward(x, w32)
+        ctx.conf = (dilation, padding, in_slope, wdtype, bias is not None)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        x, w32 = ctx.saved_tensors
+        dil, pad, slope, wdtype, has_bias = ctx.conf
+        k = w32.shape[2]
+        dy = dy.to(torch.float32).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype)
+            dx = _run(dy, layer_t, x.shape[2])
+            if slope != 1.0:
+                dx = torch.where(x > 0, dx, dx * slope)
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype)
+        return dx, dw, db, None, None, None, None
+
+
+def supported(module: nn.Module) -> bool:
+    return (isinstance(module, nn.Conv1d) and module.stride == (1,) and module.groups == 1
+            and module.padding_mode == "zeros" and not isinstance(module.padding, str)
+            and _lib_k_ok(module.kernel_size[0], module.dilation[0]))
+
+
+def _lib_k_ok(k: int, dil: int) -> bool:
+    return k in (1, 2, 3, 4, 5, 7, 9, 11) and 64 + (k - 1) * dil <= 128
+
+
+def autocast_wdtype(device_type: str = "cuda"):
+    """MFMA operand type of the enclosing autocast region (fp16 -> WDT_F16,
+    bf16 -> WDT_BF16), or None when autocast is off."""
+    if not torch.is_autocast_enabled(device_type):
+        return None
+    dt = torch.get_autocast_dtype(device_type)
+    return {torch.float16: WDT_F16, torch.bfloat16: WDT_BF16}.get(dt)
+
+
+def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) -> torch.Tensor:
+    """``module(leaky_relu(x, in_slope))`` for an nn.Conv1d (optionally
+    legacy-weight-normed or spectral-normed).
+
+    Inside a 16-bit autocast region on a ROCm device (the reference's
+    ``fp16_run`` training, train_stft.py:165,216) this is the HIP training
+    conv with operands of the autocast dtype.  Outside autocast the reference
+    computes the conv in fp32, and so does this (torch conv): the fp32
+    training mode keeps the reference's precision.  On CPU it is the torch
+    conv."""
+    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+    if wdt is None or not supported(module):
+        if in_slope != 1.0:
+            x = F.leaky_relu(x, in_slope)
+        return module(x)
+    w = weight_norm_effective(module)
+    return Conv1dHip.apply(x, w, module.bias, module.dilation[0], module.padding[0], in_slope,
+                           wdt)
