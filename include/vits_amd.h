@@ -309,6 +309,19 @@ typedef struct vits_conv1d_wgrad_desc {
 /* 64 + (k-1)*dil > 128 or k not in {1,2,3,4,5,7,9,11})                  */
 int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, void* stream);
 
+/* WaveNet gate of WN (modules.py:139-146) / ResBlock2 (modules.py:253-255) */
+/* in training: y[b][p][t] = tanh(x[b][p][t] + g[b][p]) *                 */
+/*                           sigmoid(x[b][H+p][t] + g[b][H+p]),  p < H     */
+/* g optional ([B][>= 2H] with g_bstride).  Backward: dx [B][2H][T] and   */
+/* (optional) dg[b][c] = sum_t dx[b][c][t] as a dense [B][2H].            */
+int vits_gate_forward(const float* x, int64_t x_bstride, int32_t x_cstride, const float* g,
+                      int64_t g_bstride, float* y, int64_t y_bstride, int32_t y_cstride,
+                      int batch, int half_channels, int t_len, void* stream);
+int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t dy_cstride, const float* x,
+                       int64_t x_bstride, int32_t x_cstride, const float* g, int64_t g_bstride,
+                       float* dx, int64_t dx_bstride, int32_t dx_cstride, float* dg, int batch,
+                       int half_channels, int t_len, void* stream);
+
 /* library introspection */
 const char* vits_amd_version(void);
 int vits_amd_device_arch(char* buf, int len);

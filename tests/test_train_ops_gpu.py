@@ -149,3 +149,26 @@ def test_training_forward_autocast_hip_convs(device):
     assert torch.equal(ids_h, ids_t)
     _close(o_h, o_t, "o", tol=2e-2)
     _close(o_h, torch.from_numpy(gd["o"]), "o vs fp32 reference", tol=3e-2)
+
+
+@pytest.mark.parametrize("B,H,T,with_g", [(2, 256, 500, True), (3, 16, 1537, True), (2, 64, 77, False)])
+def test_gate_fwd_bwd(device, B, H, T, with_g):
+    """Fused WN / ResBlock2 gate and its gradient (incl. the cond gradient
+    summed over time) against torch autograd in fp32."""
+    gen = torch.Generator().manual_seed(H + T)
+    x = torch.randn(B, 2 * H, T, generator=gen)
+    g = torch.randn(B, 3 * H, generator=gen) if with_g else None   # sliced below
+    dy = torch.randn(B, H, T, generator=gen)
+    xd = x.to(device).requires_grad_(True)
+    gd = g.to(device).requires_grad_(True) if with_g else None
+    y = train_ops.GateHip.apply(xd, gd[:, H:3 * H] if with_g else None)
+    y.backward(dy.to(device))
+    xr = x.clone().requires_grad_(True)
+    gr = g.clone().requires_grad_(True) if with_g else None
+    xx = xr + gr[:, H:3 * H].unsqueeze(-1) if with_g else xr
+    yr = torch.tanh(xx[:, :H]) * torch.sigmoid(xx[:, H:])
+    yr.backward(dy)
+    _close(y, yr, "y", tol=1e-5)
+    _close(xd.grad, xr.grad, "dx", tol=1e-5)
+    if with_g:
+        _close(gd.grad, gr.grad, "dg", tol=1e-5)

@@ -183,6 +183,16 @@ _SIGS = {
         [C.c_void_p] + [C.c_int] * 4 + [C.c_void_p] + [C.c_int] * 3 + [C.c_void_p],
     ),
     "vits_conv1d_wgrad": (C.c_int, [C.POINTER(ConvWgradDesc), C.c_int, C.c_void_p]),
+    "vits_gate_forward": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32,
+         C.c_int, C.c_int, C.c_int, C.c_void_p],
+    ),
+    "vits_gate_backward": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64,
+         C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p],
+    ),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
 }

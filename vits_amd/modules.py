@@ -67,9 +67,7 @@ class WN(nn.Module):
 
     def _gate(self, x_in, g, i):
         H = self.hidden_channels
-        if g is not None:
-            x_in = x_in + g[:, i * 2 * H:(i + 1) * 2 * H].unsqueeze(-1)
-        return torch.tanh(x_in[:, :H]) * torch.sigmoid(x_in[:, H:])
+        return train_ops.gate(x_in, None if g is None else g[:, i * 2 * H:(i + 1) * 2 * H])
 
     def forward(self, x, x_mask, g=None, **kwargs):
         H = self.hidden_channels
@@ -119,9 +117,7 @@ class ResBlock2(nn.Module):
             return resblock_infer(self, x, g)
         for c1, c2, cs in zip(self.convs1, self.convs2, self.conds):
             xt = train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE)
-            xa, xb = torch.chunk(xt, 2, dim=1)
-            sa, sb = torch.chunk(cs(g), 2, dim=1)
-            xt = torch.tanh(xa + sa.unsqueeze(-1)) * torch.sigmoid(xb + sb.unsqueeze(-1))
+            xt = train_ops.gate(xt, cs(g))
             x = train_ops.conv1d(c2, xt) + x
         return x
 

@@ -123,6 +123,58 @@ class Conv1dHip(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+class GateHip(torch.autograd.Function):
+    """tanh(x[:, :H] + g[:, :H, None]) * sigmoid(x[:, H:] + g[:, H:, None])
+    (WN modules.py:139-146, ResBlock2 modules.py:253-255); g optional."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x, g):
+        B, C2, T = x.shape
+        H = C2 // 2
+        if x.stride(2) != 1:
+            x = x.contiguous()
+        if g is not None and g.stride(1) != 1:
+            g = g.contiguous()
+        y = torch.empty(B, H, T, device=x.device, dtype=torch.float32)
+        check(_lib.load().vits_gate_forward(
+            x.data_ptr(), x.stride(0), x.stride(1), None if g is None else g.data_ptr(),
+            0 if g is None else g.stride(0), y.data_ptr(), y.stride(0), y.stride(1), B, H, T,
+            _stream_ptr(x.device)), "vits_gate_forward")
+        ctx.save_for_backward(x, g)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        x, g = ctx.saved_tensors
+        B, C2, T = x.shape
+        H = C2 // 2
+        dy = dy.to(torch.float32)
+        if dy.stride(2) != 1:
+            dy = dy.contiguous()
+        dx = torch.empty(B, C2, T, device=x.device, dtype=torch.float32)
+        want_dg = g is not None and ctx.needs_input_grad[1]
+        dg = torch.empty(B, C2, device=x.device, dtype=torch.float32) if want_dg else None
+        check(_lib.load().vits_gate_backward(
+            dy.data_ptr(), dy.stride(0), dy.stride(1), x.data_ptr(), x.stride(0), x.stride(1),
+            None if g is None else g.data_ptr(), 0 if g is None else g.stride(0), dx.data_ptr(),
+            dx.stride(0), dx.stride(1), None if dg is None else dg.data_ptr(), B, H, T,
+            _stream_ptr(x.device)), "vits_gate_backward")
+        return dx, dg
+
+
+def gate(x: torch.Tensor, g) -> torch.Tensor:
+    """The WN / ResBlock2 gate: the HIP op inside a 16-bit autocast region on
+    a ROCm device (where the convs around it are HIP too), torch otherwise."""
+    if x.device.type == "cuda" and autocast_wdtype() is not None:
+        return GateHip.apply(x, g)
+    H = x.shape[1] // 2
+    if g is not None:
+        x = x + g.unsqueeze(-1)
+    return torch.tanh(x[:, :H]) * torch.sigmoid(x[:, H:])
+
+
 def supported(module: nn.Module) -> bool:
     return (isinstance(module, nn.Conv1d) and module.stride == (1,) and module.groups == 1
             and module.padding_mode == "zeros" and not isinstance(module.padding, str)
@@ -130,7 +182,7 @@ def supported(module: nn.Module) -> bool:
 
 
 def _lib_k_ok(k: int, dil: int) -> bool:
-    return k in (1, 2, 3, 4, 5, 7, 9, 11) and 64 + (k - 1) * dil <= 128
+    return k in (1, 2, 3, 4, 5, 7, 9, 11) and 64 + (k - 1) * dil + 3 <= 128
 
 
 def autocast_wdtype(device_type: str = "cuda"):
