@@ -71,25 +71,12 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)ua | ((uint32_t)ub << 16);
 }
 
-template <int NK, int WT, bool V4>
-__global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(
-    const vits_conv1d_wgrad_desc p, int tchunks, int total_chunks, int chunks_per_wg, int n_ci,
-    int n_co, int n_wg, int per_xcd) {
+template <int NK, int WT>
+__global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_conv1d_wgrad_desc p,
+                                                                     int tchunks, int total_chunks,
+                                                                     int chunks_per_wg) {
   typedef typename Op16<WT>::V8 V8;
-  typedef float f32x4v __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
-  // (id % 8), so logical tile idx = xcd * per_xcd + (id / 8) gives each XCD a
-  // contiguous range, inside which the co tiles of one (split, ci tile) are
-  // adjacent and stage the same X window through that XCD's L2.
-  const int L = blockIdx.x;
-  const int idx = (L & 7) * per_xcd + (L >> 3);
-  if (idx >= n_wg) return;  // whole workgroup, before any barrier
-  const int co_t = idx % n_co;
-  const int rest = idx / n_co;
-  const int ci_t = rest % n_ci;
-  const int split = rest / n_ci;
-
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -97,34 +84,32 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(
   const int lhi = lane >> 5;
   const int wm = (wid >> 1) * 32;  // wave's co offset in the tile
   const int wn = (wid & 1) * 32;   // wave's ci offset in the tile
-  const int m0 = co_t * WG_M;
-  const int c0 = ci_t * WG_N;
-  const int ch_begin = split * chunks_per_wg;
+  const int m0 = blockIdx.z * WG_M;
+  const int c0 = blockIdx.y * WG_N;
+  const int ch_begin = blockIdx.x * chunks_per_wg;
   const int ch_end = min(total_chunks, ch_begin + chunks_per_wg);
   const int dil = p.dil;
-  const int sh = (-p.pad_left) & 3;        // window start t0 - pad, 4-aligned down by sh
-  const int wrs = KT + (NK - 1) * dil + sh;  // staged window rows (<= MAX_WR)
+  const int wr = KT + (NK - 1) * dil;  // staged window rows
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
-  const bool do_bias = p.dbias != nullptr && ci_t == 0;
+  const bool do_bias = p.dbias != nullptr && blockIdx.y == 0;
 
   f32x16 acc[NK];
 #pragma unroll
   for (int j = 0; j < NK; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  float bsum[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bsum[q] = 0.f;
 
   // ---- staging maps (fixed per thread) ------------------------------------
-  // dY: 16-byte column dyc (t = t0 + 4 dyc) of rows (tid >> 4) + 16 q, q < 4
-  const int dyc = tid & 15;
-  const int dyr = tid >> 4;
-  // X: 16-byte column xc (window rows 4 xc .. 4 xc + 3) of the channel pair
-  //    (2 cp, 2 cp + 1), cp = (tid >> 5) + 8 q, q < 4; a wave instruction
-  //    reads 512 contiguous bytes of two channel rows
-  const int xc = tid & 31;
-  const int xcp = tid >> 5;
-  const bool xcol_ok = 4 * xc < wrs;
+  // dY: pair e = tid + 256 q -> row (e >> 5), columns 2 (e & 31) + {0, 1}
+  const int dy_row0 = tid >> 5;   // + 8 q
+  const int dy_col = 2 * (tid & 31);
+  // X: wave w stages channel pairs (2 (w + 4 i), +1), i < 8, window rows
+  // lane + 64 h, h < 2: every global load instruction reads 64 consecutive
+  // time steps of one channel row (256 B).
   float dyv[16];
   float xv[32];
 
@@ -132,68 +117,54 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(
     const int b = chunk / tchunks;
     const int t0 = (chunk - b * tchunks) * KT;
     const float* dyb = p.dy + (int64_t)b * p.dy_bstride;
-    const int t = t0 + 4 * dyc;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int co = m0 + dyr + 16 * q;
-      const float* src = dyb + (int64_t)(co < p.cout ? co : 0) * p.dy_cstride + t;
-      if (V4 && co < p.cout && t + 3 < p.n_out) {
-        const f32x4v v = *reinterpret_cast<const f32x4v*>(src);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dyv[4 * q + e] = v[e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dyv[4 * q + e] = (co < p.cout && t + e < p.n_out) ? src[e] : 0.f;
-      }
+    for (int q = 0; q < 8; ++q) {
+      const int co = m0 + dy_row0 + 8 * q;
+      const int t = t0 + dy_col;
+      const float* src = dyb + (int64_t)co * p.dy_cstride + t;
+      const bool rok = co < p.cout;
+      dyv[2 * q] = (rok && t < p.n_out) ? src[0] : 0.f;
+      dyv[2 * q + 1] = (rok && t + 1 < p.n_out) ? src[1] : 0.f;
     }
     const float* xb = p.x + (int64_t)b * p.x_bstride;
-    const int tx = t0 - p.pad_left - sh + 4 * xc;
+    const int ts = t0 - p.pad_left;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int i = 0; i < 8; ++i) {
+      const int ci = c0 + 2 * (wid + 4 * i);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int ci = c0 + 2 * (xcp + 8 * q) + h;
-        const bool rok = xcol_ok && ci < p.cin;
-        const float* src = xb + (int64_t)(rok ? ci : 0) * p.x_cstride + tx;
-        float* dst = xv + (q * 2 + h) * 4;
-        if (V4 && rok && tx >= 0 && tx + 3 < p.tin) {
-          const f32x4v v = *reinterpret_cast<const f32x4v*>(src);
+        const int r = lane + 64 * h;
+        const int t = ts + r;
+        const bool tok = r < wr && t >= 0 && t < p.tin;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) dst[e] = v[e];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            dst[e] = (rok && tx + e >= 0 && tx + e < p.tin) ? src[e] : 0.f;
+        for (int e = 0; e < 2; ++e) {
+          const bool ok = tok && ci + e < p.cin;
+          xv[(i * 2 + h) * 2 + e] = ok ? xb[(int64_t)(ci + e) * p.x_cstride + t] : 0.f;
         }
       }
     }
   };
   auto lstore = [&](uint16_t* st) {
+    uint32_t* dyl = reinterpret_cast<uint32_t*>(st);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float* v = dyv + 4 * q;
-      if (do_bias) bsum[q] += (v[0] + v[1]) + (v[2] + v[3]);
-      uint2 w2;
-      w2.x = pack2<WT>(v[0], v[1]);
-      w2.y = pack2<WT>(v[2], v[3]);
-      *reinterpret_cast<uint2*>(st + (dyr + 16 * q) * DY_LD + 4 * dyc) = w2;
+    for (int q = 0; q < 8; ++q) {
+      const float a = dyv[2 * q], bv = dyv[2 * q + 1];
+      if (do_bias) bsum[q] += a + bv;
+      dyl[((dy_row0 + 8 * q) * DY_LD + dy_col) >> 1] = pack2<WT>(a, bv);
     }
-    if (xcol_ok) {
-      uint32_t* xl = reinterpret_cast<uint32_t*>(st + DY_HALVES);
+    uint32_t* xl = reinterpret_cast<uint32_t*>(st + DY_HALVES);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float* v0 = xv + (q * 2) * 4;
-        const float* v1 = v0 + 4;
-        const int cl = 2 * (xcp + 8 * q);
+    for (int i = 0; i < 8; ++i) {
+      const int cl = 2 * (wid + 4 * i);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float a = v0[e], bb = v1[e];
-          if (act_in) {
-            a = a < 0.f ? a * slope : a;
-            bb = bb < 0.f ? bb * slope : bb;
-          }
-          xl[((4 * xc + e) * X_LD + cl) >> 1] = pack2<WT>(a, bb);
+      for (int h = 0; h < 2; ++h) {
+        const int r = lane + 64 * h;
+        float v0 = xv[(i * 2 + h) * 2], v1 = xv[(i * 2 + h) * 2 + 1];
+        if (act_in) {
+          v0 = v0 < 0.f ? v0 * slope : v0;
+          v1 = v1 < 0.f ? v1 * slope : v1;
         }
+        if (h == 0 || r < wr) xl[(r * X_LD + cl) >> 1] = pack2<WT>(v0, v1);
       }
     }
   };
@@ -201,13 +172,12 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(
   // ---- fragment addressing --------------------------------------------------
   // A (dY rows): lane -> co row wm + l32, t = 16 s + 8 lhi .. + 7
   // B (tap j): 16-lane group g = lane >> 4 reads ci columns wn + 16 (g & 1) + 4 pp
-  //   (pp = lane & 3) of window rows sh + 16 s + 8 (g >> 1) + qq (+4) + j dil
-  //   (qq = (lane >> 2) & 3)
+  //   (pp = lane & 3) of rows 16 s + 8 (g >> 1) + qq (+4) + j dil (qq = (lane >> 2) & 3)
   const int g = lane >> 4;
   const int qq = (lane >> 2) & 3;
   const int pp = lane & 3;
   const int a_off = (wm + l32) * DY_LD + 8 * lhi;
-  const int b_off = DY_HALVES + (sh + 8 * (g >> 1) + qq) * X_LD + wn + 16 * (g & 1) + 4 * pp;
+  const int b_off = DY_HALVES + (8 * (g >> 1) + qq) * X_LD + wn + 16 * (g & 1) + 4 * pp;
 
   if (ch_begin < ch_end) {
     gload(ch_begin);
@@ -254,12 +224,12 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(
   }
   if (do_bias) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 8; ++q) {
       float v = bsum[q];
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
-      const int co = m0 + dyr + 16 * q;
-      if (dyc == 0 && co < p.cout) unsafeAtomicAdd(p.dbias + co, v);
+      for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+      const int co = m0 + dy_row0 + 8 * q;
+      if ((tid & 31) == 0 && co < p.cout) unsafeAtomicAdd(p.dbias + co, v);
     }
   }
 }
@@ -268,33 +238,20 @@ template <int WT>
 int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s) {
   const int tchunks = (d.n_out + KT - 1) / KT;
   const int total = batch * tchunks;
-  const int n_co = (d.cout + WG_M - 1) / WG_M;
-  const int n_ci = (d.cin + WG_N - 1) / WG_N;
-  const int tiles = n_co * n_ci;
+  const int tiles = ((d.cout + WG_M - 1) / WG_M) * ((d.cin + WG_N - 1) / WG_N);
   // >= 16 chunks (1024 time steps) per workgroup: 512 FLOP per atomic byte;
   // beyond that, about 1024 workgroups
   int cpw = (int)(((int64_t)total * tiles + 1023) / 1024);
   const int min_cpw = total < 16 ? total : 16;
   if (cpw < min_cpw) cpw = min_cpw;
   const int splits = (total + cpw - 1) / cpw;
-  const int n_wg = splits * tiles;
-  const int per_xcd = (n_wg + 7) / 8;
-  const bool v4 = (d.dy_cstride & 3) == 0 && (d.dy_bstride & 3) == 0 && (d.x_cstride & 3) == 0 &&
-                  (d.x_bstride & 3) == 0 && (reinterpret_cast<uintptr_t>(d.dy) & 15) == 0 &&
-                  (reinterpret_cast<uintptr_t>(d.x) & 15) == 0;
-  dim3 grid(8 * per_xcd);
+  dim3 grid(splits, (d.cin + WG_N - 1) / WG_N, (d.cout + WG_M - 1) / WG_M);
   const size_t lds = 2 * STAGE_HALVES * sizeof(uint16_t);
-#define VITS_WG_LAUNCH(NK, V)                                                                 \
-  hipLaunchKernelGGL((wgrad_kernel<NK, WT, V>), grid, dim3(256), lds, s, d, tchunks, total, cpw, \
-                     n_ci, n_co, n_wg, per_xcd)
-#define VITS_WG_CASE(NK)          \
-  case NK:                        \
-    if (v4)                       \
-      VITS_WG_LAUNCH(NK, true);   \
-    else                          \
-      VITS_WG_LAUNCH(NK, false);  \
-    break;
   switch (d.k) {
+#define VITS_WG_CASE(NK) \
+  case NK:               \
+    hipLaunchKernelGGL((wgrad_kernel<NK, WT>), grid, dim3(256), lds, s, d, tchunks, total, cpw); \
+    break;
     VITS_WG_CASE(1)
     VITS_WG_CASE(2)
     VITS_WG_CASE(3)
@@ -303,11 +260,10 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s) {
     VITS_WG_CASE(7)
     VITS_WG_CASE(9)
     VITS_WG_CASE(11)
+#undef VITS_WG_CASE
     default:
       return VITS_E_UNSUP;
   }
-#undef VITS_WG_CASE
-#undef VITS_WG_LAUNCH
   return vits_launch_status();
 }
 
@@ -346,7 +302,7 @@ extern "C" int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, voi
   VITS_CHECK_ARG(d->dy && d->x && d->dw_t);
   VITS_CHECK_ARG(batch > 0 && d->cout > 0 && d->cin > 0 && d->k > 0 && d->dil > 0);
   VITS_CHECK_SHAPE(d->n_out > 0 && d->tin > 0);
-  if (KT + (d->k - 1) * d->dil + 3 > MAX_WR) return VITS_E_UNSUP;
+  if (KT + (d->k - 1) * d->dil > MAX_WR) return VITS_E_UNSUP;
   if (d->wdtype == VITS_WDT_F16) return wgrad_dispatch<VITS_WDT_F16>(*d, batch, as_stream(stream));
   if (d->wdtype == VITS_WDT_BF16) return wgrad_dispatch<VITS_WDT_BF16>(*d, batch, as_stream(stream));
   return VITS_E_ARG;

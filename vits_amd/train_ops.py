@@ -182,7 +182,7 @@ def supported(module: nn.Module) -> bool:
 
 
 def _lib_k_ok(k: int, dil: int) -> bool:
-    return k in (1, 2, 3, 4, 5, 7, 9, 11) and 64 + (k - 1) * dil + 3 <= 128
+    return k in (1, 2, 3, 4, 5, 7, 9, 11) and 64 + (k - 1) * dil <= 128
 
 
 def autocast_wdtype(device_type: str = "cuda"):
