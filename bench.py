@@ -318,18 +318,30 @@ def train_leg(args, device, rank, world, dist):
     hps = default_hps()
     torch.manual_seed(hps.train.seed)
     net_g, net_d = build_models(hps, device)
-    st = TrainStep(hps, net_g, net_d, device, ddp=world > 1)
+    # single process: the whole step replayed from one hipGraph (TrainStep.capture;
+    # DDP's hooks are not capturable, so ranks > 1 run the step eagerly)
+    use_graph = world == 1 and not args.train_eager
+    st = TrainStep(hps, net_g, net_d, device, ddp=world > 1, capturable=use_graph)
     B = args.train_batch
     batch = [t.to(device) for t in synthetic_batch(hps, B, tx=args.tx, ty=args.ty, seed=rank)]
+    graph_err = None
+    if use_graph:
+        try:
+            st.capture(batch, warmup=max(1, args.train_warmup))
+        except Exception as e:  # report and time the eager step instead
+            graph_err = f"{type(e).__name__}: {e}"[:300]
+            use_graph = False
+            torch.cuda.synchronize()
+    run = (lambda: st.replay()) if use_graph else (lambda: st.step(batch))
     for _ in range(args.train_warmup):
-        st.step(batch)
+        run()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.train_steps):
-        out = st.step(batch)
+        out = run()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -346,9 +358,12 @@ def train_leg(args, device, rank, world, dist):
            "workload": f"train_stft step (G fwd/bwd + MWSD D x3 + MR-STFT + MAS) batch={B}/GPU "
                        f"Tx={args.tx} Ty={args.ty} segment 48 frames",
            "parallelism": f"ddp{world} (RCCL all-reduce)" if world > 1 else "single GPU",
+           "graph": use_graph,
            "tflops_alg": round(365.4e9 * utt / el / 1e12, 2),
            "loss_gen_all": round(float(out["loss_gen_all"]), 4),
            "reference_cpu": "0.945 utt/s at B=4 on 8 vCPU (BASELINE.md, measured in the survey)"}
+    if graph_err:
+        res["graph_error"] = graph_err
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = train_cpu_baseline()
     del st, net_g, net_d
@@ -371,6 +386,8 @@ def main():
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--train-warmup", type=int, default=2)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--train-eager", action="store_true",
+                    help="time the eager train step instead of the captured hipGraph")
     ap.add_argument("--no-longform", action="store_true")
     ap.add_argument("--no-kernels", action="store_true")
     args = ap.parse_args()

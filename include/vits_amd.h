@@ -322,6 +322,11 @@ int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t dy_cstride, 
                        float* dx, int64_t dx_bstride, int32_t dx_cstride, float* dg, int batch,
                        int half_channels, int t_len, void* stream);
 
+/* if (*flag != 0) copy, for each job i, jobs[3i+2] floats from jobs[3i+1] to */
+/* jobs[3i] (device array of int64 triples: dst, src, count); no-op else.  */
+/* GradScaler's skip rule for the graph-captured train step (train.py).    */
+int vits_masked_copy_multi(const int64_t* jobs, int njobs, const float* flag, void* stream);
+
 /* library introspection */
 const char* vits_amd_version(void);
 int vits_amd_device_arch(char* buf, int len);

@@ -65,14 +65,14 @@ def _patch_cpu():
     ops.stft_mag = _cpu_stft_mag
 
 
-def _make(hps, device, ddp=False, seed=0):
+def _make(hps, device, ddp=False, seed=0, capturable=False):
     from vits_amd.train import TrainStep, build_models
 
     torch.manual_seed(seed)
     net_g, net_d = build_models(hps, device)
     # the logging mels need hop <= n_fft; the tiny config (n_fft 64, hop 192)
     # skips them, the base-config train bench (tools/train_bench.py) runs them
-    return TrainStep(hps, net_g, net_d, device, ddp=ddp, log_mels=False)
+    return TrainStep(hps, net_g, net_d, device, ddp=ddp, log_mels=False, capturable=capturable)
 
 
 def _batch(hps, n, seed):
@@ -249,3 +249,46 @@ def test_grouped_spectral_norm_matches_torch_hooks():
         assert torch.allclose(p.grad, gr[k].grad, rtol=1e-10, atol=1e-14), k
     for k, v in d.state_dict().items():
         assert torch.allclose(v, r.state_dict()[k], rtol=1e-12, atol=1e-15), k
+
+
+@pytest.mark.gpu
+def test_train_step_graph_capture_and_skip_rule(device):
+    """The whole step captured into one hipGraph (TrainStep.capture): replays
+    train (finite losses, parameters move, the device-side alignment noise
+    decays) and GradScaler's skip rule holds without a host sync - with an
+    overflowing loss scale every gradient is inf, so neither optimizer may
+    touch its parameters or moments and the scale must back off."""
+    from vits_amd import commons
+
+    hps = tiny_hps()
+    st = _make(hps, device, capturable=True)
+    # a small initial scale so the first replays are not skipped for fp16
+    # overflow (GradScaler starts at 2**16 and halves per overflowing step)
+    st.scaler = torch.amp.GradScaler("cuda", init_scale=64.0)
+    batch = [t.to(device) for t in _batch(hps, 4, seed=0)]
+    try:
+        st.capture(batch, warmup=2)
+        g_p = [p.detach().clone() for p in st.net_g.parameters()]
+        d_p = [p.detach().clone() for p in st.net_d.parameters()]
+        an0 = float(st.net_g.__dict__["_align_noise_t"])
+        outs = [{k: v.clone() for k, v in st.replay().items()} for _ in range(3)]
+        torch.cuda.synchronize()
+        for out in outs:
+            assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
+        assert any(not torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
+        assert any(not torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
+        assert float(st.net_g.__dict__["_align_noise_t"]) < an0
+        # force overflow: every step must be skipped
+        st.scaler._scale.fill_(3.0e38)
+        g_p = [p.detach().clone() for p in st.net_g.parameters()]
+        d_p = [p.detach().clone() for p in st.net_d.parameters()]
+        d_m = [st.optim_d.state[p]["exp_avg"].clone() for p in st.net_d.parameters()]
+        st.replay()
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
+        assert all(torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
+        assert all(torch.equal(a, st.optim_d.state[p]["exp_avg"])
+                   for a, p in zip(d_m, st.net_d.parameters()))
+        assert float(st.scaler._scale) < 3.0e38
+    finally:
+        commons.DEVICE_SLICE_RNG = False

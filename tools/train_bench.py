@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--no-mels", action="store_true")
     ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--torch-prof", default=None, help="write a torch.profiler op table here")
+    ap.add_argument("--graph", action="store_true", help="capture the step into a hipGraph")
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="torch.backends.cudnn.benchmark = True (train_stft.py:26)")
     args = ap.parse_args()
@@ -31,24 +32,31 @@ def main():
     hps = default_hps()
     torch.manual_seed(1234)
     g, d = build_models(hps, dev)
-    st = TrainStep(hps, g, d, dev, log_mels=not args.no_mels, fused_adamw=not args.no_fused)
+    st = TrainStep(hps, g, d, dev, log_mels=not args.no_mels, fused_adamw=not args.no_fused,
+                   capturable=args.graph)
     batch = [t.to(dev) for t in synthetic_batch(hps, args.batch, seed=0)]
+    if args.graph:
+        t0 = time.perf_counter()
+        st.capture(batch)
+        torch.cuda.synchronize()
+        print(f"capture: {time.perf_counter() - t0:.3f}s", flush=True)
+    step = (lambda b: st.replay()) if args.graph else st.step
     for i in range(args.warmup):
         t0 = time.perf_counter()
-        st.step(batch)
+        step(batch)
         torch.cuda.synchronize()
         print(f"warmup {i}: {time.perf_counter() - t0:.3f}s", flush=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = st.step(batch)
+        out = step(batch)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     if args.torch_prof:
         from torch.profiler import ProfilerActivity, profile
 
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
-            st.step(batch)
+            step(batch)
             torch.cuda.synchronize()
         ka = prof.key_averages()
         with open(args.torch_prof, "w") as f:

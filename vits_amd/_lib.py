@@ -193,6 +193,7 @@ _SIGS = {
         [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64,
          C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p],
     ),
+    "vits_masked_copy_multi": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
 }

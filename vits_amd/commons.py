@@ -80,8 +80,19 @@ def rand_slice_segments(x: torch.Tensor, x_lengths=None, segment_size: int = 4):
     if x_lengths is None:
         x_lengths = t
     ids_str_max = x_lengths - segment_size + 1
-    ids_str = (torch.rand([b]).to(device=x.device) * ids_str_max).to(dtype=torch.long)
+    if DEVICE_SLICE_RNG:
+        # graph-captured training step (vits_amd.train.TrainStep.capture): the
+        # draw must come from the device generator so every replay re-draws
+        r = torch.rand([b], device=x.device)
+    else:
+        r = torch.rand([b]).to(device=x.device)
+    ids_str = (r * ids_str_max).to(dtype=torch.long)
     return slice_segments(x, ids_str, segment_size), ids_str
+
+
+# set by TrainStep.capture (hipGraph-captured step): rand_slice_segments then
+# draws its window starts on the device instead of the host generator
+DEVICE_SLICE_RNG = False
 
 
 def gen_sin_table(max_len: int, d_model: int, padding_idx=None) -> torch.Tensor:
@@ -97,7 +108,7 @@ def gen_sin_table(max_len: int, d_model: int, padding_idx=None) -> torch.Tensor:
     return pe.unsqueeze_(0)
 
 
-def clip_grad_value_(parameters, clip_value, norm_type=2):
+def clip_grad_value_(parameters, clip_value, norm_type=2, as_tensor=False):
     """Clamp grads to +-clip_value and return the total grad norm
     (commons.py:158-173).  The reference syncs the host once per parameter
     (.item() in the loop); here the norm is reduced on the device and read
@@ -107,7 +118,7 @@ def clip_grad_value_(parameters, clip_value, norm_type=2):
     parameters = [p for p in parameters if p.grad is not None]
     norm_type = float(norm_type)
     if not parameters:
-        return 0.0
+        return torch.zeros(()) if as_tensor else 0.0
     grads = [p.grad.detach() for p in parameters]
     if norm_type == 2.0 and grads[0].is_cuda:
         # one multi-tensor launch per dtype/device group instead of one per parameter
@@ -119,7 +130,8 @@ def clip_grad_value_(parameters, clip_value, norm_type=2):
         cv = float(clip_value)
         torch._foreach_clamp_min_(grads, -cv)
         torch._foreach_clamp_max_(grads, cv)
-    return float(total.item())
+    # as_tensor: stay on the device (no host sync: the graph-captured step)
+    return total if as_tensor else float(total.item())
 
 
 def subsequent_mask(length: int) -> torch.Tensor:

@@ -333,7 +333,14 @@ class SynthesizerTrn(nn.Module):
             neg_cent = neg_cent_scores(z_p, m_p, logs_p)
             if self.align_noise > 0:
                 eps = noise_align if noise_align is not None else torch.randn_like(neg_cent)
-                neg_cent = neg_cent + torch.std(neg_cent) * eps * self.align_noise
+                an = self.__dict__.get("_align_noise_t")
+                if an is not None:
+                    # graph-captured step: the decaying scale lives on the device
+                    # and decays inside the graph (one step per replay)
+                    neg_cent = neg_cent + torch.std(neg_cent) * eps * an
+                    an.sub_(self.align_noise_decay).clamp_(min=self.align_noise_min)
+                else:
+                    neg_cent = neg_cent + torch.std(neg_cent) * eps * self.align_noise
                 self.align_noise -= self.align_noise_decay
                 self.align_noise = max(self.align_noise, self.align_noise_min)
             attn_mask = torch.unsqueeze(x_mask, 2) * torch.unsqueeze(y_mask, -1)

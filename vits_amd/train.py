@@ -27,7 +27,8 @@ import torch
 import torch.distributed as dist
 from torch.nn.parallel import DistributedDataParallel as DDP
 
-from . import commons, utils
+from . import _lib, commons, utils
+from ._lib import check
 from .discriminators import MultiWaveSTFTDiscriminator
 from .losses import discriminator_loss, generator_loss, kl_loss
 from .mel_processing import mel_spectrogram_torch, spec_to_mel_torch
@@ -45,24 +46,34 @@ def build_models(hps, device):
 
 
 class TrainStep:
-    def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True, fused_adamw=True):
+    def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True, fused_adamw=True,
+                 capturable=False):
         self.hps = hps
         self.device = device
         self.log_mels = log_mels
+        # capturable: optimizer steps and the GradScaler skip rule stay on the
+        # device (no host sync), so the whole step can be captured (capture())
+        self.capturable = bool(capturable) and device.type == "cuda"
+        self.graph = None
+        self._d_restore = None
         self.mstft = MultiResolutionSTFTLoss().to(device)
         self.optim_g = torch.optim.AdamW(net_g.parameters(), hps.train.learning_rate,
                                          betas=hps.train.betas, weight_decay=hps.train.weight_decay,
                                          eps=hps.train.eps,
-                                         fused=fused_adamw and device.type == "cuda")
-        self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4)
+                                         fused=fused_adamw and device.type == "cuda",
+                                         capturable=self.capturable)
+        self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4, capturable=self.capturable)
         if ddp:
             ids = [device.index] if device.type == "cuda" else None
             net_g = DDP(net_g, device_ids=ids)
             net_d = DDP(net_d, device_ids=ids)
         self.net_g, self.net_d = net_g, net_d
         fp16 = bool(hps.train.fp16_run) and device.type == "cuda"
+        # the autocast weight-cast cache must be off under graph capture (cached
+        # fp16 weight copies would outlive / escape the captured region)
+        cache = not self.capturable
         self.autocast = lambda enabled=fp16: torch.autocast(device.type, dtype=torch.float16,
-                                                            enabled=enabled)
+                                                            enabled=enabled, cache_enabled=cache)
         self.scaler = torch.amp.GradScaler(device.type, enabled=fp16)
 
     def step(self, batch):
@@ -92,8 +103,12 @@ class TrainStep:
         self.optim_d.zero_grad()
         self.scaler.scale(loss_disc).backward()
         self.scaler.unscale_(self.optim_d)
-        grad_norm_d = commons.clip_grad_value_(self.net_d.parameters(), None)
-        self.scaler.step(self.optim_d)
+        grad_norm_d = commons.clip_grad_value_(self.net_d.parameters(), None,
+                                               as_tensor=self.capturable)
+        if self.capturable:
+            self._step_d_sync_free()
+        else:
+            self.scaler.step(self.optim_d)
 
         with self.autocast():
             y_d_hat_g = self.net_d(y_hat, y_hat_mag)
@@ -107,12 +122,114 @@ class TrainStep:
         self.optim_g.zero_grad()
         self.scaler.scale(loss_gen_all).backward()
         self.scaler.unscale_(self.optim_g)
-        grad_norm_g = commons.clip_grad_value_(self.net_g.parameters(), None)
+        grad_norm_g = commons.clip_grad_value_(self.net_g.parameters(), None,
+                                               as_tensor=self.capturable)
         self.scaler.step(self.optim_g)
         self.scaler.update()
         return {"loss_disc": loss_disc.detach(), "loss_gen_all": loss_gen_all.detach(),
                 "loss_stft": loss_stft.detach(), "loss_dur": loss_dur.detach(),
                 "loss_kl": loss_kl.detach(), "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
+
+    def _step_d_sync_free(self):
+        """GradScaler.step for the (non-fused) RAdam without its host sync:
+        the step always runs and is then undone on the device when the
+        unscale found an inf/NaN (params, moments and step count restored
+        from a backup by a masked copy), which is GradScaler's skip rule
+        (torch/amp/grad_scaler.py step())."""
+        opt = self.optim_d
+        if not self.scaler.is_enabled():
+            opt.step()
+            return
+        found = sum(self.scaler._per_optimizer_states[id(opt)]["found_inf_per_device"].values())
+        if self._d_restore is None:
+            self._init_d_restore()
+        cur, backup, jobs = self._d_restore
+        with torch.no_grad():
+            torch._foreach_copy_(backup, cur)
+            opt.step()
+            flag = found.to(torch.float32)
+            check(_lib.load().vits_masked_copy_multi(jobs.data_ptr(), len(cur), flag.data_ptr(),
+                                                     torch.cuda.current_stream(self.device).cuda_stream),
+                  "vits_masked_copy_multi")
+
+    def _init_d_restore(self):
+        """RAdam state created up front (same fields torch creates lazily on
+        the first step, capturable layout) and a persistent backup of params
+        + moments + step counters with the device job table of the masked
+        restore.  Built before any capture (it copies a host table)."""
+        opt = self.optim_d
+        for group in opt.param_groups:
+            for p in group["params"]:
+                st = opt.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        ps = [p for g in opt.param_groups for p in g["params"]]
+        cur = [p.detach() for p in ps]
+        for k in ("exp_avg", "exp_avg_sq", "step"):
+            cur += [opt.state[p][k] for p in ps]
+        assert all(t.dtype == torch.float32 and t.is_contiguous() for t in cur)
+        backup = [torch.empty_like(t) for t in cur]
+        table = torch.tensor([[d.data_ptr(), s.data_ptr(), d.numel()] for d, s in zip(cur, backup)],
+                             dtype=torch.int64).to(self.device)
+        self._d_restore = (cur, backup, table)
+
+    def capture(self, batch, warmup: int = 3):
+        """Capture one whole step (both forwards, both backwards, both
+        optimizer steps, the scaler update) into a hipGraph.  The batch is
+        copied into static device buffers; replay(batch) refreshes them and
+        replays.  Host-side randomness becomes device-side (rand_slice draw)
+        and the alignment-noise decay runs inside the graph.  Single process
+        only (DDP's hooks are not capturable)."""
+        assert self.capturable, "TrainStep(capturable=True) is required"
+        assert not isinstance(self.net_g, DDP), "graph capture is single-process"
+        commons.DEVICE_SLICE_RNG = True
+        g_mod = self.net_g
+        g_mod.__dict__["_align_noise_t"] = torch.tensor(float(g_mod.align_noise),
+                                                        device=self.device)
+        self.static = [t.to(self.device).clone() for t in batch]
+        self._release_autograd_refs()
+        if self._d_restore is None and self.scaler.is_enabled():
+            self._init_d_restore()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.step(self.static)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        self._release_autograd_refs()
+        self.graph = torch.cuda.CUDAGraph()
+        self.optim_g.zero_grad(set_to_none=True)
+        self.optim_d.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.static_out = self.step(self.static)
+        return self.static_out
+
+    def _release_autograd_refs(self):
+        """Weight-norm / spectral-norm modules keep the last forward's
+        computed ``weight`` (with its autograd graph) as an attribute, which
+        keeps the parameters' AccumulateGrad nodes - and the stream they were
+        created on - alive.  Eager steps on another stream before a capture
+        would then make the captured backward accumulate on that stream.
+        Drop those graphs (the hooks recompute ``weight`` every forward)."""
+        for net in (self.net_g, self.net_d):
+            for m in net.modules():
+                for name in ("weight",):
+                    if hasattr(m, name + "_g") or hasattr(m, name + "_orig"):
+                        t = m.__dict__.get(name)
+                        if isinstance(t, torch.Tensor) and t.grad_fn is not None:
+                            m.__dict__[name] = t.detach()
+
+    def replay(self, batch=None):
+        if batch is not None:
+            for dst, src in zip(self.static, batch):
+                dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        g_mod = self.net_g
+        g_mod.align_noise = max(g_mod.align_noise - g_mod.align_noise_decay, g_mod.align_noise_min)
+        return self.static_out
 
 
 def default_hps():
