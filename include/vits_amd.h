@@ -125,6 +125,13 @@ typedef struct vits_conv1d_desc {
   /* 16-bit type when staged; fp32 accumulation:                           */
   /* v_mfma_f32_32x32x16_bf16 / _f16)                                       */
   int32_t wdtype;
+  /* single-output STORE only (the input gradient of a conv whose forward   */
+  /* fused a leaky-relu prologue): v *= gmask[b][row][n] > 0 ? 1 : slope    */
+  /* before residual / accumulate; gmask = the forward's input, NULL = off  */
+  const float* gmask;
+  int64_t gmask_bstride;
+  int32_t gmask_cstride;
+  float gmask_slope;
 } vits_conv1d_desc;
 
 #define VITS_WDT_F32 0
@@ -281,8 +288,11 @@ int vits_attention_forward(const float* q, const float* k, const float* v, float
 /* wdtype (VITS_WDT_F16 / _BF16).  transpose = 0: rows = co, channels =   */
 /* ci (forward).  transpose = 1: rows = ci, channels = co, taps reversed  */
 /* (input gradient: dX = conv(dY, W', pad_left = (k-1)*dil - pad)).       */
+/* zero / zero_n: optional fp32 buffer the same launch clears (the weight- */
+/* gradient accumulator of the backward that follows; NULL / 0 = none).   */
 int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, void* out,
-                       int m_pad, int cin_pad, int wdtype, void* stream);
+                       int m_pad, int cin_pad, int wdtype, float* zero, int64_t zero_n,
+                       void* stream);
 
 typedef struct vits_conv1d_wgrad_desc {
   const float* dy;        /* output gradient [B][cout][n_out], t contiguous  */

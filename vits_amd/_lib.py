@@ -73,6 +73,10 @@ class ConvDesc(C.Structure):
         ("out0", ConvOut),
         ("out1", ConvOut),
         ("wdtype", C.c_int32),
+        ("gmask", C.c_void_p),
+        ("gmask_bstride", C.c_int64),
+        ("gmask_cstride", C.c_int32),
+        ("gmask_slope", C.c_float),
     ]
 
 
@@ -180,7 +184,8 @@ _SIGS = {
     ),
     "vits_conv1d_pack16": (
         C.c_int,
-        [C.c_void_p] + [C.c_int] * 4 + [C.c_void_p] + [C.c_int] * 3 + [C.c_void_p],
+        [C.c_void_p] + [C.c_int] * 4 + [C.c_void_p] + [C.c_int] * 3
+        + [C.c_void_p, C.c_int64, C.c_void_p],
     ),
     "vits_conv1d_wgrad": (C.c_int, [C.POINTER(ConvWgradDesc), C.c_int, C.c_void_p]),
     "vits_gate_forward": (

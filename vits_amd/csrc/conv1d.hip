@@ -39,6 +39,7 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   VITS_CHECK_ARG(d.wdtype == VITS_WDT_F32 || d.wdtype == VITS_WDT_BF16 ||
                  d.wdtype == VITS_WDT_F16);
   if (d.wdtype != VITS_WDT_F32) VITS_CHECK_SHAPE((d.kc % 16) == 0);
+  if (d.gmask) VITS_CHECK_ARG(d.epi == VITS_EPI_STORE && d.split >= d.m);
   return VITS_OK;
 }
 

@@ -472,6 +472,17 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             v[r] = apply_act(acc[mi][ni][r] + erow[rloc + (r & 3) + 8 * (r >> 2)], o0.act);
+          if (p.gmask) {  // leaky-relu derivative of the forward input
+            const float* gb = p.gmask + (int64_t)b * p.gmask_bstride + n;
+            float gv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + (r & 3) + 8 * (r >> 2);
+              gv[r] = gb[(int64_t)(row < p.m ? row : 0) * p.gmask_cstride];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = gv[r] > 0.f ? v[r] : v[r] * p.gmask_slope;
+          }
           float* yb = o0.y + (int64_t)b * o0.y_bstride + n;
           if (o0.res) {
             const float* rb = o0.res + (int64_t)b * o0.res_bstride + n;

@@ -270,7 +270,11 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s) {
 // ---- weight image for the 16-bit forward kernel ------------------------------
 template <typename T>
 __global__ void pack16_kernel(const float* __restrict__ w, int cout, int cin, int k, int transpose,
-                              T* __restrict__ out, int m_pad, int cin_pad) {
+                              T* __restrict__ out, int m_pad, int cin_pad,
+                              float* __restrict__ zero, int64_t zero_n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < zero_n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    zero[i] = 0.f;
   // out[c/16][j][(c%16)/8][m][c%8]; rows m / channels c are (co, ci) or,
   // transposed, (ci, co) with the tap order reversed
   const int64_t total = (int64_t)cin_pad * k * m_pad;
@@ -309,21 +313,24 @@ extern "C" int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, voi
 }
 
 extern "C" int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, void* out,
-                                  int m_pad, int cin_pad, int wdtype, void* stream) {
+                                  int m_pad, int cin_pad, int wdtype, float* zero, int64_t zero_n,
+                                  void* stream) {
+  VITS_CHECK_ARG(zero_n >= 0 && (zero_n == 0 || zero));
   VITS_CHECK_ARG(w && out && cout > 0 && cin > 0 && k > 0);
   const int rows = transpose ? cin : cout;
   const int chans = transpose ? cout : cin;
   VITS_CHECK_SHAPE(m_pad % 128 == 0 && m_pad >= rows && cin_pad % 16 == 0 && cin_pad >= chans);
   const int64_t total = (int64_t)cin_pad * k * m_pad;
-  const int64_t nblk = (total + 255) / 256;
+  const int64_t most = total > zero_n ? total : zero_n;
+  const int64_t nblk = (most + 255) / 256;
   const int blocks = (int)(nblk < 4096 ? nblk : 4096);
   hipStream_t s = as_stream(stream);
   if (wdtype == VITS_WDT_F16)
     hipLaunchKernelGGL(pack16_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, w, cout, cin, k,
-                       transpose, reinterpret_cast<_Float16*>(out), m_pad, cin_pad);
+                       transpose, reinterpret_cast<_Float16*>(out), m_pad, cin_pad, zero, zero_n);
   else if (wdtype == VITS_WDT_BF16)
     hipLaunchKernelGGL(pack16_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, w, cout, cin, k,
-                       transpose, reinterpret_cast<__bf16*>(out), m_pad, cin_pad);
+                       transpose, reinterpret_cast<__bf16*>(out), m_pad, cin_pad, zero, zero_n);
   else
     return VITS_E_ARG;
   return vits_launch_status();

@@ -46,35 +46,53 @@ TRAIN_WDTYPE = WDT_F16  # the reference's autocast dtype (train_stft.py:165)
 
 
 def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype: int,
-            bias: torch.Tensor | None = None) -> PackedConv:
+            bias: torch.Tensor | None = None, zero: torch.Tensor | None = None) -> PackedConv:
+    """16-bit weight image (and, in the same launch, clear ``zero``)."""
     cout, cin, k = w32.shape
     rows, chans = (cin, cout) if transpose else (cout, cin)
     m_pad = (rows + 127) // 128 * 128
     cin_pad = (chans + 15) // 16 * 16
     img = torch.empty(cin_pad // 16, k, 2, m_pad, 8, dtype=_TORCH_16[wdtype], device=w32.device)
-    check(_lib.load().vits_conv1d_pack16(w32.data_ptr(), cout, cin, k, int(transpose),
-                                         img.data_ptr(), m_pad, cin_pad, wdtype,
-                                         _stream_ptr(w32.device)), "vits_conv1d_pack16")
+    check(_lib.load().vits_conv1d_pack16(
+        w32.data_ptr(), cout, cin, k, int(transpose), img.data_ptr(), m_pad, cin_pad, wdtype,
+        None if zero is None else zero.data_ptr(), 0 if zero is None else zero.numel(),
+        _stream_ptr(w32.device)), "vits_conv1d_pack16")
     return PackedConv(img, bias, chans, rows, k, dil, pad_left, EPI_STORE,
                       _pick_tile_bf16(rows, k), 16, out_channels=rows, wdtype=wdtype)
 
 
-def _run(x: torch.Tensor, layer: PackedConv, n_out: int, in_slope: float = 1.0) -> torch.Tensor:
+def _run(x: torch.Tensor, layer: PackedConv, n_out: int, in_slope: float = 1.0,
+         gmask: torch.Tensor | None = None, gmask_slope: float = 1.0) -> torch.Tensor:
     B = x.shape[0]
     y = torch.empty(B, layer.m, n_out, device=x.device, dtype=torch.float32)
     d = make_desc(layer, x, make_out(y), in_slope=in_slope, tin=x.shape[2], n_out=n_out)
+    if gmask is not None:
+        # leaky-relu derivative of the forward input, fused into the epilogue
+        d.gmask, d.gmask_bstride, d.gmask_cstride = gmask.data_ptr(), gmask.stride(0), gmask.stride(1)
+        d.gmask_slope = gmask_slope
     conv1d_launch(d, B, x.device)
     return y
 
 
+def wgrad_buffer(cout: int, cin: int, k: int, with_bias: bool, device, zeroed: bool = True):
+    """One fp32 accumulator for [k][cout][cin] dW (+ [cout] dbias)."""
+    n = k * cout * cin + (cout if with_bias else 0)
+    alloc = torch.zeros if zeroed else torch.empty
+    return alloc(n, device=device, dtype=torch.float32)
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, k: int, dil: int, pad_left: int,
-          in_slope: float = 1.0, with_bias: bool = True, wdtype: int = TRAIN_WDTYPE):
-    """dW [Cout, Cin, k] and dbias [Cout] (fp32) of y = conv1d(act(x), W) + b."""
+          in_slope: float = 1.0, with_bias: bool = True, wdtype: int = TRAIN_WDTYPE,
+          buf: torch.Tensor | None = None):
+    """dW [Cout, Cin, k] and dbias [Cout] (fp32) of y = conv1d(act(x), W) + b.
+    ``buf``: a zeroed wgrad_buffer (else one is allocated)."""
     B, cout, n_out = dy.shape
     _, cin, tin = x.shape
     assert dy.stride(2) == 1 and x.stride(2) == 1 and dy.dtype == x.dtype == torch.float32
-    dw_t = torch.zeros(k, cout, cin, device=dy.device, dtype=torch.float32)
-    db = torch.zeros(cout, device=dy.device, dtype=torch.float32) if with_bias else None
+    if buf is None:
+        buf = wgrad_buffer(cout, cin, k, with_bias, dy.device)
+    dw_t = buf[:k * cout * cin].view(k, cout, cin)
+    db = buf[k * cout * cin:] if with_bias else None
     d = ConvWgradDesc()
     d.dy, d.dy_bstride, d.dy_cstride, d.cout = dy.data_ptr(), dy.stride(0), dy.stride(1), cout
     d.x, d.x_bstride, d.x_cstride, d.cin = x.data_ptr(), x.stride(0), x.stride(1), cin
@@ -84,6 +102,8 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, k: int, dil: int, pad_left: int,
     d.dbias = None if db is None else db.data_ptr()
     d.wdtype = wdtype
     check(_lib.load().vits_conv1d_wgrad(d, B, _stream_ptr(dy.device)), "vits_conv1d_wgrad")
+    if k == 1:  # [1][cout][cin] is already the parameter layout
+        return dw_t.view(cout, cin, 1), db
     return dw_t.permute(1, 2, 0).contiguous(), db
 
 
@@ -112,14 +132,18 @@ class Conv1dHip(torch.autograd.Function):
         dil, pad, slope, wdtype, has_bias = ctx.conf
         k = w32.shape[2]
         dy = dy.to(torch.float32).contiguous()
-        dx = dw = db = None
+        dx = dw = db = buf = None
+        cout, cin = w32.shape[0], w32.shape[1]
+        want_w = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
         if ctx.needs_input_grad[0]:
-            layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype)
-            dx = _run(dy, layer_t, x.shape[2])
-            if slope != 1.0:
-                dx = torch.where(x > 0, dx, dx * slope)
-        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype)
+            # the weight-gradient accumulator is cleared by the packing launch
+            if want_w:
+                buf = wgrad_buffer(cout, cin, k, has_bias, dy.device, zeroed=False)
+            layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, zero=buf)
+            dx = _run(dy, layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
+                      gmask_slope=slope)
+        if want_w:
+            dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype, buf=buf)
         return dx, dw, db, None, None, None, None
 
 
