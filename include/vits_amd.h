@@ -332,10 +332,24 @@ int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t dy_cstride, 
                        float* dx, int64_t dx_bstride, int32_t dx_cstride, float* dg, int batch,
                        int half_channels, int t_len, void* stream);
 
-/* if (*flag != 0) copy, for each job i, jobs[3i+2] floats from jobs[3i+1] to */
-/* jobs[3i] (device array of int64 triples: dst, src, count); no-op else.  */
-/* GradScaler's skip rule for the graph-captured train step (train.py).    */
-int vits_masked_copy_multi(const int64_t* jobs, int njobs, const float* flag, void* stream);
+/* Fused RAdam step (radam.py:35-99, the D optimizer of train_stft.py:97) */
+/* over a list of fp32 tensors, one launch per VITS_RADAM_MAX tensors.     */
+/* scal: device float[8] state (scal[0] = step count, the rest scratch);  */
+/* found_inf: device flag of GradScaler's unscale (NULL = never skip);    */
+/* when set, nothing is updated (GradScaler's skip rule, no host sync).   */
+/* grad_scale: device scalar the grads are still multiplied by (NULL =    */
+/* already unscaled).                                                     */
+#define VITS_RADAM_MAX 96
+typedef struct vits_radam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+} vits_radam_tensor;
+int vits_radam_step(const vits_radam_tensor* tensors, int n, float* scal, const float* found_inf,
+                    const float* grad_scale, double lr, double beta1, double beta2, double eps,
+                    double weight_decay, void* stream);
 
 /* library introspection */
 const char* vits_amd_version(void);

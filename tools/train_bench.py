@@ -56,13 +56,17 @@ def main():
         from torch.profiler import ProfilerActivity, profile
 
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
-            step(batch)
+            st.step(batch)  # eager, so ops and step: phases are attributed
             torch.cuda.synchronize()
         ka = prof.key_averages()
         with open(args.torch_prof, "w") as f:
             f.write(ka.table(sort_by="self_cuda_time_total", row_limit=60, max_name_column_width=90))
             f.write("\n\n")
             f.write(ka.table(sort_by="cuda_time_total", row_limit=60, max_name_column_width=90))
+            f.write("\n\n")
+            phases = [e for e in ka if e.key.startswith("step:")]
+            for e in sorted(phases, key=lambda e: -e.device_time_total):
+                f.write(f"{e.key:32s} device {e.device_time_total / 1e3:8.2f} ms  cpu {e.cpu_time_total / 1e3:8.2f} ms\n")
     print(json.dumps({"batch": args.batch, "s_per_step": dt, "utt_per_s": args.batch / dt,
                       "loss_g": float(out["loss_gen_all"]), "loss_d": float(out["loss_disc"]),
                       "max_mem_gb": torch.cuda.max_memory_allocated() / 2**30}), flush=True)

@@ -123,6 +123,19 @@ class ConvWgradDesc(C.Structure):
     ]
 
 
+RADAM_MAX = 96
+
+
+class RadamTensor(C.Structure):
+    _fields_ = [
+        ("param", C.c_void_p),
+        ("grad", C.c_void_p),
+        ("exp_avg", C.c_void_p),
+        ("exp_avg_sq", C.c_void_p),
+        ("numel", C.c_int64),
+    ]
+
+
 _SIGS = {
     "vits_conv1d_forward": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_void_p]),
     "vits_conv1d_forward_seq": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_int, C.c_void_p]),
@@ -198,7 +211,11 @@ _SIGS = {
         [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64,
          C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p],
     ),
-    "vits_masked_copy_multi": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "vits_radam_step": (
+        C.c_int,
+        [C.POINTER(RadamTensor), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        + [C.c_double] * 5 + [C.c_void_p],
+    ),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
 }

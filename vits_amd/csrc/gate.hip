@@ -105,31 +105,3 @@ extern "C" int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t d
                      dx_bstride, dx_cstride, dg, half_channels, t_len);
   return vits_launch_status();
 }
-
-// ---------------------------------------------------------------------------
-// Masked multi-tensor copy: when *flag != 0, dst_i <- src_i for every job i
-// (one launch for all tensors; nothing is touched when the flag is 0).  The
-// graph-captured training step uses it for GradScaler's skip rule on the
-// non-fused RAdam: the step always runs and is undone from a backup when the
-// unscale found an inf/NaN (a select, so NaN results cannot leak through).
-// ---------------------------------------------------------------------------
-namespace {
-__global__ __launch_bounds__(256) void masked_copy_kernel(const int64_t* __restrict__ jobs,
-                                                         const float* __restrict__ flag) {
-  if (*flag == 0.f) return;
-  const int64_t* j = jobs + 3 * blockIdx.y;
-  float* dst = reinterpret_cast<float*>(j[0]);
-  const float* src = reinterpret_cast<const float*>(j[1]);
-  const int64_t n = j[2];
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    dst[i] = src[i];
-}
-}  // namespace
-
-extern "C" int vits_masked_copy_multi(const int64_t* jobs, int njobs, const float* flag,
-                                      void* stream) {
-  VITS_CHECK_ARG(jobs && flag && njobs > 0 && njobs <= 65535);
-  hipLaunchKernelGGL(masked_copy_kernel, dim3(64, njobs), dim3(256), 0, as_stream(stream), jobs,
-                     flag);
-  return vits_launch_status();
-}

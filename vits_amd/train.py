@@ -13,8 +13,11 @@ all-reduce over RCCL/xGMI (the ``nccl`` backend on ROCm).
 Differences from the reference, all on the host side: per-discriminator
 losses stay on the device (no ``.item()`` per loss, losses.py:28-29) and the
 grad norm is reduced on the device once (commons.py:158-173 syncs per
-parameter); RAdam is ``torch.optim.RAdam`` (same rectified-Adam update as
-radam.py).
+parameter); the D optimizer is radam.py's RAdam as one fused HIP launch
+(vits_amd.optim.FusedRAdam, GradScaler-aware without a host sync).
+
+``capture()`` records the whole step into one hipGraph (single process):
+the step is then GPU-bound instead of bound by ~14k host-side launches.
 """
 from __future__ import annotations
 
@@ -27,12 +30,12 @@ import torch
 import torch.distributed as dist
 from torch.nn.parallel import DistributedDataParallel as DDP
 
-from . import _lib, commons, utils
-from ._lib import check
+from . import commons, utils
 from .discriminators import MultiWaveSTFTDiscriminator
 from .losses import discriminator_loss, generator_loss, kl_loss
 from .mel_processing import mel_spectrogram_torch, spec_to_mel_torch
 from .models import SynthesizerTrn
+from .optim import FusedRAdam
 from .stft_loss import MultiResolutionSTFTLoss
 
 
@@ -55,14 +58,18 @@ class TrainStep:
         # device (no host sync), so the whole step can be captured (capture())
         self.capturable = bool(capturable) and device.type == "cuda"
         self.graph = None
-        self._d_restore = None
         self.mstft = MultiResolutionSTFTLoss().to(device)
         self.optim_g = torch.optim.AdamW(net_g.parameters(), hps.train.learning_rate,
                                          betas=hps.train.betas, weight_decay=hps.train.weight_decay,
                                          eps=hps.train.eps,
                                          fused=fused_adamw and device.type == "cuda",
                                          capturable=self.capturable)
-        self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4, capturable=self.capturable)
+        # radam.py's RAdam (train_stft.py:97): one fused HIP launch on the GPU
+        # (GradScaler-aware, sync-free); torch's RAdam (same update) on CPU
+        if device.type == "cuda":
+            self.optim_d = FusedRAdam(net_d.parameters(), 1e-4)
+        else:
+            self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4)
         if ddp:
             ids = [device.index] if device.type == "cuda" else None
             net_g = DDP(net_g, device_ids=ids)
@@ -78,102 +85,66 @@ class TrainStep:
 
     def step(self, batch):
         hps = self.hps
+        rf = torch.profiler.record_function  # phase labels for torch.profiler tables
         x, x_lengths, spec, spec_lengths, y, y_lengths, emo, speakers = (
             t.to(self.device, non_blocking=True) for t in batch)
         with self.autocast():
-            (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
-             (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
-                x, x_lengths, spec, spec_lengths, emo, speakers)
+            with rf("step:G.forward"):
+                (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
+                 (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
+                    x, x_lengths, spec, spec_lengths, emo, speakers)
             if self.log_mels:  # train_stft.py:173-191 (logging mels, computed every step)
-                mel = spec_to_mel_torch(spec[:1].float(), hps.data.filter_length,
-                                        hps.data.n_mel_channels, hps.data.sampling_rate,
-                                        hps.data.mel_fmin, hps.data.mel_fmax)
-                _ = commons.slice_segments(mel, ids_slice[:1], hps.train.segment_size // hps.data.hop_length)
-                with torch.no_grad():
-                    _ = mel_spectrogram_torch(y_hat[:1].squeeze(1).detach().float(), hps.data.filter_length,
-                                              hps.data.n_mel_channels, hps.data.sampling_rate,
-                                              hps.data.hop_length, hps.data.win_length,
-                                              hps.data.mel_fmin, hps.data.mel_fmax)
-            y = commons.slice_segments(y, ids_slice * hps.data.hop_length, hps.train.segment_size)
-            sc_loss, mag_loss, y_mag, y_hat_mag = self.mstft(y.squeeze(1), y_hat.squeeze(1))
-            y_d_hat_r = self.net_d(y, y_mag)
-            y_d_hat_g = self.net_d(y_hat.detach(), [m.detach() for m in y_hat_mag])
-            with self.autocast(False):
-                loss_disc, _, _ = discriminator_loss(y_d_hat_r, y_d_hat_g)
-        self.optim_d.zero_grad()
-        self.scaler.scale(loss_disc).backward()
-        self.scaler.unscale_(self.optim_d)
-        grad_norm_d = commons.clip_grad_value_(self.net_d.parameters(), None,
-                                               as_tensor=self.capturable)
-        if self.capturable:
-            self._step_d_sync_free()
-        else:
+                with rf("step:log_mels"):
+                    mel = spec_to_mel_torch(spec[:1].float(), hps.data.filter_length,
+                                            hps.data.n_mel_channels, hps.data.sampling_rate,
+                                            hps.data.mel_fmin, hps.data.mel_fmax)
+                    _ = commons.slice_segments(mel, ids_slice[:1],
+                                               hps.train.segment_size // hps.data.hop_length)
+                    with torch.no_grad():
+                        _ = mel_spectrogram_torch(y_hat[:1].squeeze(1).detach().float(),
+                                                  hps.data.filter_length, hps.data.n_mel_channels,
+                                                  hps.data.sampling_rate, hps.data.hop_length,
+                                                  hps.data.win_length, hps.data.mel_fmin,
+                                                  hps.data.mel_fmax)
+            with rf("step:mrstft"):
+                y = commons.slice_segments(y, ids_slice * hps.data.hop_length, hps.train.segment_size)
+                sc_loss, mag_loss, y_mag, y_hat_mag = self.mstft(y.squeeze(1), y_hat.squeeze(1))
+            with rf("step:D.forward(real,fake)"):
+                y_d_hat_r = self.net_d(y, y_mag)
+                y_d_hat_g = self.net_d(y_hat.detach(), [m.detach() for m in y_hat_mag])
+                with self.autocast(False):
+                    loss_disc, _, _ = discriminator_loss(y_d_hat_r, y_d_hat_g)
+        with rf("step:D.backward"):
+            self.optim_d.zero_grad()
+            self.scaler.scale(loss_disc).backward()
+        with rf("step:D.optimizer"):
+            self.scaler.unscale_(self.optim_d)
+            grad_norm_d = commons.clip_grad_value_(self.net_d.parameters(), None,
+                                                   as_tensor=self.capturable)
             self.scaler.step(self.optim_d)
 
         with self.autocast():
-            y_d_hat_g = self.net_d(y_hat, y_hat_mag)
-            with self.autocast(False):
+            with rf("step:D.forward(gen)"):
+                y_d_hat_g = self.net_d(y_hat, y_hat_mag)
+            with rf("step:G.losses"), self.autocast(False):
                 loss_dur = torch.sum(l_length.float()) * hps.train.c_dur
                 loss_stft = (sc_loss.float() + mag_loss.float()) * hps.train.c_stft
                 loss_kl = kl_loss(z_p, logs_q, m_p, logs_p, z_mask) * hps.train.c_kl
                 loss_kl_q = kl_loss(z_q, logs_p, m_q, logs_q, z_mask) * hps.train.c_kl_q
                 loss_gen, _ = generator_loss(y_d_hat_g)
                 loss_gen_all = loss_gen + loss_stft + loss_dur + loss_kl + loss_kl_q
-        self.optim_g.zero_grad()
-        self.scaler.scale(loss_gen_all).backward()
-        self.scaler.unscale_(self.optim_g)
-        grad_norm_g = commons.clip_grad_value_(self.net_g.parameters(), None,
-                                               as_tensor=self.capturable)
-        self.scaler.step(self.optim_g)
-        self.scaler.update()
+        with rf("step:G.backward"):
+            self.optim_g.zero_grad()
+            self.scaler.scale(loss_gen_all).backward()
+        with rf("step:G.optimizer"):
+            self.scaler.unscale_(self.optim_g)
+            grad_norm_g = commons.clip_grad_value_(self.net_g.parameters(), None,
+                                                   as_tensor=self.capturable)
+            self.scaler.step(self.optim_g)
+            self.scaler.update()
         return {"loss_disc": loss_disc.detach(), "loss_gen_all": loss_gen_all.detach(),
                 "loss_stft": loss_stft.detach(), "loss_dur": loss_dur.detach(),
                 "loss_kl": loss_kl.detach(), "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
-
-    def _step_d_sync_free(self):
-        """GradScaler.step for the (non-fused) RAdam without its host sync:
-        the step always runs and is then undone on the device when the
-        unscale found an inf/NaN (params, moments and step count restored
-        from a backup by a masked copy), which is GradScaler's skip rule
-        (torch/amp/grad_scaler.py step())."""
-        opt = self.optim_d
-        if not self.scaler.is_enabled():
-            opt.step()
-            return
-        found = sum(self.scaler._per_optimizer_states[id(opt)]["found_inf_per_device"].values())
-        if self._d_restore is None:
-            self._init_d_restore()
-        cur, backup, jobs = self._d_restore
-        with torch.no_grad():
-            torch._foreach_copy_(backup, cur)
-            opt.step()
-            flag = found.to(torch.float32)
-            check(_lib.load().vits_masked_copy_multi(jobs.data_ptr(), len(cur), flag.data_ptr(),
-                                                     torch.cuda.current_stream(self.device).cuda_stream),
-                  "vits_masked_copy_multi")
-
-    def _init_d_restore(self):
-        """RAdam state created up front (same fields torch creates lazily on
-        the first step, capturable layout) and a persistent backup of params
-        + moments + step counters with the device job table of the masked
-        restore.  Built before any capture (it copies a host table)."""
-        opt = self.optim_d
-        for group in opt.param_groups:
-            for p in group["params"]:
-                st = opt.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-        ps = [p for g in opt.param_groups for p in g["params"]]
-        cur = [p.detach() for p in ps]
-        for k in ("exp_avg", "exp_avg_sq", "step"):
-            cur += [opt.state[p][k] for p in ps]
-        assert all(t.dtype == torch.float32 and t.is_contiguous() for t in cur)
-        backup = [torch.empty_like(t) for t in cur]
-        table = torch.tensor([[d.data_ptr(), s.data_ptr(), d.numel()] for d, s in zip(cur, backup)],
-                             dtype=torch.int64).to(self.device)
-        self._d_restore = (cur, backup, table)
 
     def capture(self, batch, warmup: int = 3):
         """Capture one whole step (both forwards, both backwards, both
@@ -190,8 +161,6 @@ class TrainStep:
                                                         device=self.device)
         self.static = [t.to(self.device).clone() for t in batch]
         self._release_autograd_refs()
-        if self._d_restore is None and self.scaler.is_enabled():
-            self._init_d_restore()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
