@@ -22,6 +22,7 @@ the step is then GPU-bound instead of bound by ~14k host-side launches.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import os
 import sys
 import time
@@ -123,7 +124,17 @@ class TrainStep:
                                                    as_tensor=self.capturable)
             self.scaler.step(self.optim_d)
 
-        with self.autocast():
+        # The generator loss backpropagates through D only for dL/dy_hat: D's
+        # own weight gradients from this backward are discarded by the next
+        # optim_d.zero_grad() (train_stft.py:202-232), so they are not computed
+        # (identical updates, ~1/3 less D backward work).
+        # Under DDP the D pass runs in no_sync() (no all-reduce of D grads that
+        # nobody uses; the reference pays for it).
+        d_params = [p for p in self.net_d.parameters() if p.requires_grad]
+        for p in d_params:
+            p.requires_grad_(False)
+        d_ctx = self.net_d.no_sync() if isinstance(self.net_d, DDP) else contextlib.nullcontext()
+        with self.autocast(), d_ctx:
             with rf("step:D.forward(gen)"):
                 y_d_hat_g = self.net_d(y_hat, y_hat_mag)
             with rf("step:G.losses"), self.autocast(False):
@@ -136,6 +147,8 @@ class TrainStep:
         with rf("step:G.backward"):
             self.optim_g.zero_grad()
             self.scaler.scale(loss_gen_all).backward()
+        for p in d_params:
+            p.requires_grad_(True)
         with rf("step:G.optimizer"):
             self.scaler.unscale_(self.optim_g)
             grad_norm_g = commons.clip_grad_value_(self.net_g.parameters(), None,
