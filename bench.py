@@ -318,10 +318,13 @@ def train_leg(args, device, rank, world, dist):
     hps = default_hps()
     torch.manual_seed(hps.train.seed)
     net_g, net_d = build_models(hps, device)
-    # single process: the whole step replayed from one hipGraph (TrainStep.capture;
-    # DDP's hooks are not capturable, so ranks > 1 run the step eagerly)
-    use_graph = world == 1 and not args.train_eager
-    st = TrainStep(hps, net_g, net_d, device, ddp=world > 1, capturable=use_graph)
+    # the whole step replayed from one hipGraph (TrainStep.capture); with
+    # several ranks the gradient average is one flat RCCL all-reduce per
+    # network captured in the graph (allreduce=True; DDP's hooks are not
+    # capturable, so the eager path keeps DDP)
+    use_graph = not args.train_eager
+    st = TrainStep(hps, net_g, net_d, device, ddp=world > 1 and not use_graph,
+                   capturable=use_graph, allreduce=world > 1 and use_graph)
     B = args.train_batch
     batch = [t.to(device) for t in synthetic_batch(hps, B, tx=args.tx, ty=args.ty, seed=rank)]
     graph_err = None
@@ -357,7 +360,8 @@ def train_leg(args, device, rank, world, dist):
            "scaling": "weak",
            "workload": f"train_stft step (G fwd/bwd + MWSD D x3 + MR-STFT + MAS) batch={B}/GPU "
                        f"Tx={args.tx} Ty={args.ty} segment 48 frames",
-           "parallelism": f"ddp{world} (RCCL all-reduce)" if world > 1 else "single GPU",
+           "parallelism": (f"dp{world} (flat RCCL all-reduce per network)" if st.allreduce else
+                           f"ddp{world} (RCCL all-reduce)") if world > 1 else "single GPU",
            "graph": use_graph,
            "tflops_alg": round(365.4e9 * utt / el / 1e12, 2),
            "loss_gen_all": round(float(out["loss_gen_all"]), 4),

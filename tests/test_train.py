@@ -65,14 +65,15 @@ def _patch_cpu():
     ops.stft_mag = _cpu_stft_mag
 
 
-def _make(hps, device, ddp=False, seed=0, capturable=False):
+def _make(hps, device, ddp=False, seed=0, capturable=False, allreduce=False):
     from vits_amd.train import TrainStep, build_models
 
     torch.manual_seed(seed)
     net_g, net_d = build_models(hps, device)
     # the logging mels need hop <= n_fft; the tiny config (n_fft 64, hop 192)
     # skips them, the base-config train bench (tools/train_bench.py) runs them
-    return TrainStep(hps, net_g, net_d, device, ddp=ddp, log_mels=False, capturable=capturable)
+    return TrainStep(hps, net_g, net_d, device, ddp=ddp, log_mels=False, capturable=capturable,
+                     allreduce=allreduce)
 
 
 def _batch(hps, n, seed):
@@ -171,13 +172,15 @@ def _free_port():
     return port
 
 
-def _ddp_worker(rank, world, port, out_dir):
+def _ddp_worker(rank, world, port, out_dir, mode="ddp"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     _patch_cpu()
     hps = tiny_hps()
-    st = _make(hps, torch.device("cpu"), ddp=True, seed=0)
+    # different init per rank: the allreduce mode must broadcast rank 0's
+    st = _make(hps, torch.device("cpu"), ddp=mode == "ddp", seed=0 if mode == "ddp" else rank,
+               allreduce=mode == "allreduce")
     for i in range(2):
         out = st.step(_batch(hps, 2, seed=10 * i + rank))  # different data per rank
     flat = torch.cat([p.detach().flatten() for p in st.net_g.parameters()] +
@@ -187,9 +190,12 @@ def _ddp_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_ddp_gloo_world2_replicas_stay_identical(tmp_path):
+@pytest.mark.parametrize("mode", ["ddp", "allreduce"])
+def test_ddp_gloo_world2_replicas_stay_identical(tmp_path, mode):
+    """Both multi-process modes (DDP; the graph-capturable flat all-reduce)
+    keep the replicas bit-identical while each rank sees different data."""
     port = _free_port()
-    mp.spawn(_ddp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_ddp_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
     a = np.load(tmp_path / "rank0.npy")
     b = np.load(tmp_path / "rank1.npy")
     assert np.array_equal(a, b)  # gradient all-reduce -> identical updates

@@ -51,7 +51,13 @@ def build_models(hps, device):
 
 class TrainStep:
     def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True, fused_adamw=True,
-                 capturable=False):
+                 capturable=False, allreduce=False):
+        """ddp: wrap both networks in DDP (eager steps).  allreduce: the
+        graph-capturable alternative for multi-process runs - no DDP hooks;
+        rank 0's parameters/buffers are broadcast once and each network's
+        gradients are averaged after its backward with one flat RCCL
+        all-reduce (the same averaged-gradient semantics as DDP)."""
+        assert not (ddp and allreduce)
         self.hps = hps
         self.device = device
         self.log_mels = log_mels
@@ -75,6 +81,13 @@ class TrainStep:
             ids = [device.index] if device.type == "cuda" else None
             net_g = DDP(net_g, device_ids=ids)
             net_d = DDP(net_d, device_ids=ids)
+        self.allreduce = bool(allreduce) and dist.is_available() and dist.is_initialized()
+        self._flat = {}
+        if self.allreduce:
+            with torch.no_grad():
+                for net in (net_g, net_d):
+                    for t in list(net.parameters()) + list(net.buffers()):
+                        dist.broadcast(t, src=0)
         self.net_g, self.net_d = net_g, net_d
         fp16 = bool(hps.train.fp16_run) and device.type == "cuda"
         # the autocast weight-cast cache must be off under graph capture (cached
@@ -118,6 +131,8 @@ class TrainStep:
         with rf("step:D.backward"):
             self.optim_d.zero_grad()
             self.scaler.scale(loss_disc).backward()
+            if self.allreduce:
+                self._allreduce_grads("d", self.net_d)
         with rf("step:D.optimizer"):
             self.scaler.unscale_(self.optim_d)
             grad_norm_d = commons.clip_grad_value_(self.net_d.parameters(), None,
@@ -147,6 +162,8 @@ class TrainStep:
         with rf("step:G.backward"):
             self.optim_g.zero_grad()
             self.scaler.scale(loss_gen_all).backward()
+            if self.allreduce:
+                self._allreduce_grads("g", self.net_g)
         for p in d_params:
             p.requires_grad_(True)
         with rf("step:G.optimizer"):
@@ -159,15 +176,42 @@ class TrainStep:
                 "loss_stft": loss_stft.detach(), "loss_dur": loss_dur.detach(),
                 "loss_kl": loss_kl.detach(), "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
 
+    def _allreduce_grads(self, key, net):
+        """Average this network's gradients over the ranks: one flat buffer,
+        one all-reduce (RCCL over xGMI on ROCm; capturable), copies in and
+        out as multi-tensor launches.  Every rank has the same set of
+        parameters with gradients (identical graphs), so the layout agrees."""
+        ps = [p for p in net.parameters() if p.grad is not None]
+        if not ps:
+            return
+        ent = self._flat.get(key)
+        if ent is None or ent[0] != [id(p) for p in ps]:
+            n = sum(p.numel() for p in ps)
+            flat = torch.empty(n, device=ps[0].device, dtype=torch.float32)
+            views, o = [], 0
+            for p in ps:
+                views.append(flat[o:o + p.numel()].view_as(p))
+                o += p.numel()
+            ent = ([id(p) for p in ps], flat, views)
+            self._flat[key] = ent
+        _, flat, views = ent
+        grads = [p.grad for p in ps]
+        torch._foreach_copy_(views, grads)
+        dist.all_reduce(flat)
+        flat.div_(dist.get_world_size())
+        torch._foreach_copy_(grads, views)
+
     def capture(self, batch, warmup: int = 3):
         """Capture one whole step (both forwards, both backwards, both
         optimizer steps, the scaler update) into a hipGraph.  The batch is
         copied into static device buffers; replay(batch) refreshes them and
         replays.  Host-side randomness becomes device-side (rand_slice draw)
-        and the alignment-noise decay runs inside the graph.  Single process
-        only (DDP's hooks are not capturable)."""
+        and the alignment-noise decay runs inside the graph.  Multi-process
+        runs capture with allreduce=True (the gradient all-reduce becomes a
+        captured RCCL node); DDP's hooks are not capturable."""
         assert self.capturable, "TrainStep(capturable=True) is required"
-        assert not isinstance(self.net_g, DDP), "graph capture is single-process"
+        assert not isinstance(self.net_g, DDP), \
+            "DDP's hooks are not capturable: use TrainStep(allreduce=True) for multi-process capture"
         commons.DEVICE_SLICE_RNG = True
         g_mod = self.net_g
         g_mod.__dict__["_align_noise_t"] = torch.tensor(float(g_mod.align_noise),
@@ -185,7 +229,9 @@ class TrainStep:
         self.graph = torch.cuda.CUDAGraph()
         self.optim_g.zero_grad(set_to_none=True)
         self.optim_d.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph):
+        # thread_local: the process-group watchdog thread keeps querying its
+        # (pre-capture) events while this thread captures
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.static_out = self.step(self.static)
         return self.static_out
 
