@@ -265,7 +265,7 @@ def kernels_leg(device):
     }
 
 
-def train_cpu_baseline(steps=2, B=4):
+def train_cpu_baseline(budget_s=10.0, B=4, max_steps=50):
     """The same train_stft step on the host cores (BASELINE.md measured the
     reference at B=4 on 8 vCPU): vits_amd.train.TrainStep on CPU with the
     three HIP-only ops swapped for CPU restatements -- MAS from
@@ -300,8 +300,10 @@ def train_cpu_baseline(steps=2, B=4):
         batch = synthetic_batch(hps, B, seed=0)
         st.step(batch)  # warm-up
         t0 = time.perf_counter()
-        for _ in range(steps):
+        steps = 0
+        while steps < max_steps and (steps < 2 or time.perf_counter() - t0 < budget_s):
             st.step(batch)
+            steps += 1
         el = time.perf_counter() - t0
     finally:
         vm.maximum_path, vm.neg_cent_scores, ops.stft_mag = saved
