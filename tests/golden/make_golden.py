@@ -17,6 +17,11 @@ Fixtures (npz, float32 unless noted):
                       (the external package is absent: SURVEY.md §8(c)).
   base_state_dict_shapes.json   reference state_dict keys -> shapes (drop-in
                       checkpoint contract).
+  mpd.npz             models.MultiPeriodDiscriminator (train.py's D) on
+                      y, y_hat [2, 1, 1201]: every score, per-feature-map
+                      sums / abs-sums / shapes, discriminator / generator /
+                      feature losses, d(loss_gen + loss_fm)/dy_hat;
+                      mpd_state_dict_shapes.json its keys -> shapes.
   mrstft.npz          stft_loss.MultiResolutionSTFTLoss on x,y [2, 9216]:
                       sc, mag, magnitude maps of resolutions 0 and 4
                       (utterance 0), per-resolution sums, d(sc+mag)/dy_hat.
@@ -212,12 +217,45 @@ def make_mrstft(stft_loss):
     np.savez_compressed(os.path.join(HERE, "mrstft.npz"), **arrs)
 
 
+def make_mpd(models):
+    import losses
+
+    d = models.MultiPeriodDiscriminator(False)
+    deterministic_fill_(d)
+    with open(os.path.join(HERE, "mpd_state_dict_shapes.json"), "w") as f:
+        json.dump({k: list(v.shape) for k, v in d.state_dict().items()}, f, indent=0)
+    g = torch.Generator().manual_seed(7)
+    # 1201 samples: not a multiple of any period (reflect-pad path of every P)
+    y = (torch.randn(2, 1, 1201, generator=g) * 0.3).clamp(-1, 1)
+    y_hat = (torch.randn(2, 1, 1201, generator=g) * 0.3).clamp(-1, 1).requires_grad_(True)
+    y_d_rs, y_d_gs, fmap_rs, fmap_gs = d(y, y_hat)
+    loss_disc, _, _ = losses.discriminator_loss(y_d_rs, [t.detach() for t in y_d_gs])
+    loss_fm = losses.feature_loss(fmap_rs, fmap_gs)
+    loss_gen, _ = losses.generator_loss(y_d_gs)
+    (loss_gen + loss_fm).backward()
+    arrs = dict(y=np32(y), y_hat=np32(y_hat.detach()), loss_disc=np32(loss_disc),
+                loss_fm=np32(loss_fm), loss_gen=np32(loss_gen), grad_y_hat=np32(y_hat.grad))
+    for i in range(len(y_d_rs)):
+        arrs[f"r{i}"] = np32(y_d_rs[i])
+        arrs[f"g{i}"] = np32(y_d_gs[i])
+        for j, (a, b) in enumerate(zip(fmap_rs[i], fmap_gs[i])):
+            arrs[f"fr{i}_{j}_shape"] = np.array(a.shape, np.int64)
+            arrs[f"fr{i}_{j}_sum"] = np.float64(a.double().sum())
+            arrs[f"fr{i}_{j}_abs"] = np.float64(a.double().abs().sum())
+            arrs[f"fg{i}_{j}_sum"] = np.float64(b.double().sum())
+    np.savez_compressed(os.path.join(HERE, "mpd.npz"), **arrs)
+
+
 def main():
     torch.set_num_threads(8)
     models, stft_loss = _ref()
+    if len(sys.argv) > 1 and sys.argv[1] == "mpd":  # only the MPD fixture
+        make_mpd(models)
+        return
     make_base(models)
     make_tiny(models)
     make_mrstft(stft_loss)
+    make_mpd(models)
     with open(os.path.join(HERE, "tiny_config.json"), "w") as f:
         json.dump(dict(model=TINY, data=TINY_DATA), f, indent=1)
     print("golden fixtures written to", HERE)

@@ -65,15 +65,26 @@ def _patch_cpu():
     ops.stft_mag = _cpu_stft_mag
 
 
-def _make(hps, device, ddp=False, seed=0, capturable=False, allreduce=False):
+def tiny_mel_hps():
+    """tiny_hps for train.py's variant: the mel-L1 loss needs hop <= n_fft,
+    so the spectrogram is 512-point (257 channels) with the reference's
+    hop 192; c_mel 45 as configs/base.json."""
+    hps = tiny_hps()
+    hps.data.filter_length = 512
+    hps.data.win_length = 512
+    hps.train.c_mel = 45
+    return hps
+
+
+def _make(hps, device, ddp=False, seed=0, capturable=False, allreduce=False, variant="stft"):
     from vits_amd.train import TrainStep, build_models
 
     torch.manual_seed(seed)
-    net_g, net_d = build_models(hps, device)
+    net_g, net_d = build_models(hps, device, variant)
     # the logging mels need hop <= n_fft; the tiny config (n_fft 64, hop 192)
     # skips them, the base-config train bench (tools/train_bench.py) runs them
     return TrainStep(hps, net_g, net_d, device, ddp=ddp, log_mels=False, capturable=capturable,
-                     allreduce=allreduce)
+                     allreduce=allreduce, variant=variant)
 
 
 def _batch(hps, n, seed):
@@ -164,6 +175,42 @@ def test_train_step_cpu_reduces_loss_and_updates(monkeypatch):
     assert changed > 50
 
 
+def test_train_step_mel_variant_cpu(monkeypatch):
+    """train.py's loop (MultiPeriodDiscriminator, mel-L1, feature matching,
+    AdamW for D) on CPU: finite losses, both networks updated."""
+    import vits_amd.models as vm
+    import vits_amd.ops as ops
+    from vits_amd.models import MultiPeriodDiscriminator
+
+    monkeypatch.setattr(vm, "maximum_path", _cpu_mas)
+    monkeypatch.setattr(vm, "neg_cent_scores", _cpu_neg_cent)
+    monkeypatch.setattr(ops, "stft_mag", _cpu_mel_stft_mag)
+    hps = tiny_mel_hps()
+    st = _make(hps, torch.device("cpu"), variant="mel")
+    assert isinstance(st.net_d, MultiPeriodDiscriminator)
+    assert isinstance(st.optim_d, torch.optim.AdamW)
+    batch = _batch(hps, 2, seed=0)
+    g0 = {n: p.detach().clone() for n, p in st.net_g.named_parameters()}
+    d0 = {n: p.detach().clone() for n, p in st.net_d.named_parameters()}
+    out = st.step(batch)
+    for k in ("loss_disc", "loss_gen_all", "loss_mel", "loss_fm", "loss_dur", "loss_kl"):
+        assert torch.isfinite(out[k]), k
+    assert out["loss_mel"] > 0 and out["loss_fm"] > 0
+    assert sum(not torch.equal(g0[n], p) for n, p in st.net_g.named_parameters()) > 50
+    assert sum(not torch.equal(d0[n], p) for n, p in st.net_d.named_parameters()) > 20
+
+
+def _cpu_mel_stft_mag(x, window, n_fft, hop, win, pad=None, eps=1e-7):
+    """stft_mag with the explicit reflect pad + center=False of
+    mel_processing.spectrogram_torch (torch.stft on CPU)."""
+    if pad is None:
+        return _cpu_stft_mag(x, window, n_fft, hop, win, eps=eps)
+    xp = torch.nn.functional.pad(x.float().unsqueeze(1), (pad, pad), mode="reflect").squeeze(1)
+    spec = torch.stft(xp, n_fft, hop, win, window.to(x.device), center=False,
+                      return_complex=True)
+    return torch.sqrt(spec.real ** 2 + spec.imag ** 2 + eps)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -213,6 +260,35 @@ def test_train_step_gpu_fp16(device):
     for out in outs:
         assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
     assert st.scaler.is_enabled()
+
+
+@pytest.mark.gpu
+def test_train_step_mel_variant_gpu_eager_and_graph(device):
+    """train.py's variant on the HIP path: eager steps, then the whole step
+    captured into one hipGraph and replayed (finite losses, D and G move)."""
+    from vits_amd import commons
+
+    hps = tiny_mel_hps()
+    st = _make(hps, device, variant="mel")
+    batch = [t.to(device) for t in _batch(hps, 4, seed=0)]
+    outs = [st.step(batch) for _ in range(2)]
+    torch.cuda.synchronize()
+    for out in outs:
+        assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_mel"])
+    st = _make(hps, device, variant="mel", capturable=True)
+    st.scaler = torch.amp.GradScaler("cuda", init_scale=64.0)
+    try:
+        st.capture(batch, warmup=2)
+        d_p = [p.detach().clone() for p in st.net_d.parameters()]
+        g_p = [p.detach().clone() for p in st.net_g.parameters()]
+        outs = [{k: v.clone() for k, v in st.replay().items()} for _ in range(3)]
+        torch.cuda.synchronize()
+        for out in outs:
+            assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
+        assert any(not torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
+        assert any(not torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
+    finally:
+        commons.DEVICE_SLICE_RNG = False
 
 
 def test_grouped_spectral_norm_matches_torch_hooks():

@@ -26,14 +26,15 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the step into a hipGraph")
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="torch.backends.cudnn.benchmark = True (train_stft.py:26)")
+    ap.add_argument("--variant", choices=["stft", "mel"], default="stft")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.backends.cudnn.benchmark = args.cudnn_benchmark
     hps = default_hps()
     torch.manual_seed(1234)
-    g, d = build_models(hps, dev)
+    g, d = build_models(hps, dev, args.variant)
     st = TrainStep(hps, g, d, dev, log_mels=not args.no_mels, fused_adamw=not args.no_fused,
-                   capturable=args.graph)
+                   capturable=args.graph, variant=args.variant)
     batch = [t.to(dev) for t in synthetic_batch(hps, args.batch, seed=0)]
     if args.graph:
         t0 = time.perf_counter()
@@ -67,7 +68,7 @@ def main():
             phases = [e for e in ka if e.key.startswith("step:")]
             for e in sorted(phases, key=lambda e: -e.device_time_total):
                 f.write(f"{e.key:32s} device {e.device_time_total / 1e3:8.2f} ms  cpu {e.cpu_time_total / 1e3:8.2f} ms\n")
-    print(json.dumps({"batch": args.batch, "s_per_step": dt, "utt_per_s": args.batch / dt,
+    print(json.dumps({"variant": args.variant, "batch": args.batch, "s_per_step": dt, "utt_per_s": args.batch / dt,
                       "loss_g": float(out["loss_gen_all"]), "loss_d": float(out["loss_disc"]),
                       "max_mem_gb": torch.cuda.max_memory_allocated() / 2**30}), flush=True)
 

@@ -18,6 +18,7 @@ from torch.nn.utils import spectral_norm, weight_norm
 from torch.nn.utils.spectral_norm import SpectralNorm
 
 from . import train_ops
+from .commons import get_padding
 
 LRELU_SLOPE = 0.2
 
@@ -186,3 +187,150 @@ class MultiWaveSTFTDiscriminator(nn.Module):
         MR-STFT loss's outputs, train_stft.py:198-199)."""
         self._sn.apply(self.training)
         return self.mwd(x) + self.mfd(m)
+
+
+# ---------------------------------------------------------------------------
+# HiFi-GAN multi-period discriminator of the train.py variant
+# (reference models.py:321-408; train.py:83,193-230)
+# ---------------------------------------------------------------------------
+
+MPD_LRELU_SLOPE = 0.1  # modules.LRELU_SLOPE (models.py:347,374)
+
+
+def _wn_weight(m: nn.Module) -> torch.Tensor:
+    """Effective weight of a legacy weight-normed conv (the pre-forward hook's
+    ``_weight_norm(v, g, 0)``), computed here because the period branch
+    calls the functional conv instead of the module."""
+    return torch._weight_norm(m.weight_v, m.weight_g, 0)
+
+
+class DiscriminatorP(nn.Module):
+    """models.py:321-355.  Same parameters and state_dict keys (``convs.i``
+    Conv2d (k, 1) weights, ``conv_post``).
+
+    A (k, 1) Conv2d over the [b, c, t/p, p] view is p independent 1-D convs
+    along t/p, so with weight norm (the default) the period branch runs in a
+    column-major 1-D layout: the waveform is regrouped once into [b*p, 1, t/p]
+    and every layer is a Conv1d over that batch (the stride-3 layers on
+    MIOpen; the stride-1 1024->1024 k5 layer and conv_post on the HIP
+    training conv under autocast).  The returned feature maps are
+    zero-copy [b, c, t', p] views of those activations, element for element
+    the reference's; the score is flattened in the reference's (t', p)
+    order.  With spectral norm the reference's 2-D module path runs as is."""
+
+    def __init__(self, period, kernel_size=5, stride=3, use_spectral_norm=False):
+        super().__init__()
+        self.period = period
+        self.use_spectral_norm = use_spectral_norm
+        norm_f = spectral_norm if use_spectral_norm else weight_norm
+        pad = (get_padding(kernel_size, 1), 0)
+        chans = [1, 32, 128, 512, 1024, 1024]
+        self.convs = nn.ModuleList([
+            norm_f(Conv2d(chans[i], chans[i + 1], (kernel_size, 1), (stride if i < 4 else 1, 1),
+                          padding=pad)) for i in range(5)])
+        self.conv_post = norm_f(Conv2d(1024, 1, (3, 1), 1, padding=(1, 0)))
+
+    def _pad(self, x):
+        b, c, t = x.shape
+        if t % self.period != 0:
+            n_pad = self.period - (t % self.period)
+            x = F.pad(x, (0, n_pad), "reflect")
+            t = t + n_pad
+        return x, t
+
+    def forward(self, x):
+        if self.use_spectral_norm:
+            return self._forward_2d(x)
+        x, t = self._pad(x)
+        b, c, p = x.shape[0], x.shape[1], self.period
+        # [b, c, t/p, p] -> [b*p, c, t/p] (one small copy of the waveform)
+        x = x.view(b, c, t // p, p).permute(0, 3, 1, 2).reshape(b * p, c, t // p)
+        fmap = []
+        for layer in self.convs:
+            w = _wn_weight(layer).squeeze(-1)
+            s, pd = layer.stride[0], layer.padding[0]
+            if s == 1 and train_ops.autocast_wdtype(x.device.type) is not None \
+                    and x.device.type == "cuda":
+                x = train_ops.Conv1dHip.apply(x, w, layer.bias, 1, pd, 1.0,
+                                              train_ops.autocast_wdtype(x.device.type))
+            else:
+                x = F.conv1d(x, w, layer.bias, stride=s, padding=pd)
+            x = F.leaky_relu(x, MPD_LRELU_SLOPE)
+            fmap.append(x.view(b, p, x.shape[1], x.shape[2]).permute(0, 2, 3, 1))
+        w = _wn_weight(self.conv_post).squeeze(-1)
+        if train_ops.autocast_wdtype(x.device.type) is not None and x.device.type == "cuda":
+            x = train_ops.Conv1dHip.apply(x, w, self.conv_post.bias, 1, 1, 1.0,
+                                          train_ops.autocast_wdtype(x.device.type))
+        else:
+            x = F.conv1d(x, w, self.conv_post.bias, padding=1)
+        x = x.view(b, p, 1, x.shape[2]).permute(0, 2, 3, 1)
+        fmap.append(x)
+        return torch.flatten(x, 1, -1), fmap
+
+    def _forward_2d(self, x):
+        x, t = self._pad(x)
+        b, c = x.shape[:2]
+        x = x.view(b, c, t // self.period, self.period)
+        fmap = []
+        for layer in self.convs:
+            x = F.leaky_relu(layer(x), MPD_LRELU_SLOPE)
+            fmap.append(x)
+        x = self.conv_post(x)
+        fmap.append(x)
+        return torch.flatten(x, 1, -1), fmap
+
+
+class DiscriminatorS(nn.Module):
+    """models.py:358-384 (grouped strided convs: torch/MIOpen; the stride-1
+    1024->1024 k5 layer and conv_post on the HIP training conv under
+    autocast when weight-normed)."""
+
+    def __init__(self, use_spectral_norm=False):
+        super().__init__()
+        norm_f = spectral_norm if use_spectral_norm else weight_norm
+        self.use_spectral_norm = use_spectral_norm
+        self.convs = nn.ModuleList([
+            norm_f(Conv1d(1, 16, 15, 1, padding=7)),
+            norm_f(Conv1d(16, 64, 41, 4, groups=4, padding=20)),
+            norm_f(Conv1d(64, 256, 41, 4, groups=16, padding=20)),
+            norm_f(Conv1d(256, 1024, 41, 4, groups=64, padding=20)),
+            norm_f(Conv1d(1024, 1024, 41, 4, groups=256, padding=20)),
+            norm_f(Conv1d(1024, 1024, 5, 1, padding=2)),
+        ])
+        self.conv_post = norm_f(Conv1d(1024, 1, 3, 1, padding=1))
+
+    def _conv(self, layer, x):
+        if not self.use_spectral_norm:
+            return train_ops.conv1d(layer, x)  # HIP when supported + autocast, else torch
+        return layer(x)
+
+    def forward(self, x):
+        fmap = []
+        for layer in self.convs:
+            x = F.leaky_relu(self._conv(layer, x), MPD_LRELU_SLOPE)
+            fmap.append(x)
+        x = self._conv(self.conv_post, x)
+        fmap.append(x)
+        return torch.flatten(x, 1, -1), fmap
+
+
+class MultiPeriodDiscriminator(nn.Module):
+    """models.py:387-408: DiscriminatorS + DiscriminatorP(2, 3, 5, 7, 11);
+    forward(y, y_hat) -> (y_d_rs, y_d_gs, fmap_rs, fmap_gs)."""
+
+    def __init__(self, use_spectral_norm=False):
+        super().__init__()
+        discs = [DiscriminatorS(use_spectral_norm=use_spectral_norm)]
+        discs += [DiscriminatorP(i, use_spectral_norm=use_spectral_norm) for i in [2, 3, 5, 7, 11]]
+        self.discriminators = nn.ModuleList(discs)
+
+    def forward(self, y, y_hat):
+        y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
+        for d in self.discriminators:
+            y_d_r, fmap_r = d(y)
+            y_d_g, fmap_g = d(y_hat)
+            y_d_rs.append(y_d_r)
+            y_d_gs.append(y_d_g)
+            fmap_rs.append(fmap_r)
+            fmap_gs.append(fmap_g)
+        return y_d_rs, y_d_gs, fmap_rs, fmap_gs

@@ -515,3 +515,8 @@ class SynthesizerTrn(nn.Module):
         run.static = static
         run.output = out
         return run
+
+
+# train.py's discriminator lives beside the generator in the reference's
+# models.py (models.py:321-408); the implementation is in discriminators.py
+from .discriminators import DiscriminatorP, DiscriminatorS, MultiPeriodDiscriminator  # noqa: E402,F401

@@ -33,31 +33,42 @@ from torch.nn.parallel import DistributedDataParallel as DDP
 
 from . import commons, utils
 from .discriminators import MultiWaveSTFTDiscriminator
-from .losses import discriminator_loss, generator_loss, kl_loss
+from .losses import discriminator_loss, feature_loss, generator_loss, kl_loss
 from .mel_processing import mel_spectrogram_torch, spec_to_mel_torch
-from .models import SynthesizerTrn
+from .models import MultiPeriodDiscriminator, SynthesizerTrn
 from .optim import FusedRAdam
 from .stft_loss import MultiResolutionSTFTLoss
 
 
-def build_models(hps, device):
+def build_models(hps, device, variant: str = "stft"):
+    """(net_g, net_d): variant "stft" = train_stft.py (MWSD discriminator,
+    train_stft.py:88-90), "mel" = train.py (MultiPeriodDiscriminator,
+    train.py:74-83)."""
     net_g = SynthesizerTrn(hps.data.text_channels, hps.data.filter_length // 2 + 1,
                            hps.train.segment_size // hps.data.hop_length,
                            n_speakers=hps.data.n_speakers, align_noise=hps.train.align_noise,
                            align_noise_decay=hps.train.align_noise_decay, **hps.model).to(device)
-    net_d = MultiWaveSTFTDiscriminator().to(device)
+    if variant == "mel":
+        net_d = MultiPeriodDiscriminator(hps.model.get("use_spectral_norm", False)).to(device)
+    else:
+        net_d = MultiWaveSTFTDiscriminator().to(device)
     return net_g, net_d
 
 
 class TrainStep:
     def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True, fused_adamw=True,
-                 capturable=False, allreduce=False):
+                 capturable=False, allreduce=False, variant: str = "stft"):
         """ddp: wrap both networks in DDP (eager steps).  allreduce: the
         graph-capturable alternative for multi-process runs - no DDP hooks;
         rank 0's parameters/buffers are broadcast once and each network's
         gradients are averaged after its backward with one flat RCCL
         all-reduce (the same averaged-gradient semantics as DDP)."""
         assert not (ddp and allreduce)
+        assert variant in ("stft", "mel"), variant
+        # "stft": train_stft.py (MWSD D + MR-STFT loss, D optimizer RAdam);
+        # "mel": train.py (MultiPeriodDiscriminator + mel-L1 + feature
+        # matching, D optimizer AdamW with weight_decay 0, train.py:93-99)
+        self.variant = variant
         self.hps = hps
         self.device = device
         self.log_mels = log_mels
@@ -73,7 +84,13 @@ class TrainStep:
                                          capturable=self.capturable)
         # radam.py's RAdam (train_stft.py:97): one fused HIP launch on the GPU
         # (GradScaler-aware, sync-free); torch's RAdam (same update) on CPU
-        if device.type == "cuda":
+        if variant == "mel":
+            self.optim_d = torch.optim.AdamW(net_d.parameters(), hps.train.learning_rate,
+                                             betas=hps.train.betas, weight_decay=0,
+                                             eps=hps.train.eps,
+                                             fused=fused_adamw and device.type == "cuda",
+                                             capturable=self.capturable)
+        elif device.type == "cuda":
             self.optim_d = FusedRAdam(net_d.parameters(), 1e-4)
         else:
             self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4)
@@ -98,6 +115,8 @@ class TrainStep:
         self.scaler = torch.amp.GradScaler(device.type, enabled=fp16)
 
     def step(self, batch):
+        if self.variant == "mel":
+            return self._step_mel(batch)
         hps = self.hps
         rf = torch.profiler.record_function  # phase labels for torch.profiler tables
         x, x_lengths, spec, spec_lengths, y, y_lengths, emo, speakers = (
@@ -175,6 +194,81 @@ class TrainStep:
         return {"loss_disc": loss_disc.detach(), "loss_gen_all": loss_gen_all.detach(),
                 "loss_stft": loss_stft.detach(), "loss_dur": loss_dur.detach(),
                 "loss_kl": loss_kl.detach(), "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
+
+    def _step_mel(self, batch):
+        """One iteration of train.py's loop (train.py:171-233; the unused
+        DurationDiscriminator branch, ``use_dur_dis``, is off in the
+        reference and its class is not defined there)."""
+        hps = self.hps
+        rf = torch.profiler.record_function
+        x, x_lengths, spec, spec_lengths, y, y_lengths, emo, speakers = (
+            t.to(self.device, non_blocking=True) for t in batch)
+        seg = hps.train.segment_size // hps.data.hop_length
+        with self.autocast():
+            with rf("step:G.forward"):
+                (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
+                 (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
+                    x, x_lengths, spec, spec_lengths, emo, speakers)
+            with rf("step:mel"):
+                mel = spec_to_mel_torch(spec.float(), hps.data.filter_length,
+                                        hps.data.n_mel_channels, hps.data.sampling_rate,
+                                        hps.data.mel_fmin, hps.data.mel_fmax)
+                y_mel = commons.slice_segments(mel, ids_slice, seg)
+                y_hat_mel = mel_spectrogram_torch(y_hat.squeeze(1).float(), hps.data.filter_length,
+                                                  hps.data.n_mel_channels, hps.data.sampling_rate,
+                                                  hps.data.hop_length, hps.data.win_length,
+                                                  hps.data.mel_fmin, hps.data.mel_fmax)
+                y = commons.slice_segments(y, ids_slice * hps.data.hop_length, hps.train.segment_size)
+            with rf("step:D.forward(real,fake)"):
+                y_d_hat_r, y_d_hat_g, _, _ = self.net_d(y, y_hat.detach())
+                with self.autocast(False):
+                    loss_disc, _, _ = discriminator_loss(y_d_hat_r, y_d_hat_g)
+        with rf("step:D.backward"):
+            self.optim_d.zero_grad()
+            self.scaler.scale(loss_disc).backward()
+            if self.allreduce:
+                self._allreduce_grads("d", self.net_d)
+        with rf("step:D.optimizer"):
+            self.scaler.unscale_(self.optim_d)
+            grad_norm_d = commons.clip_grad_value_(self.net_d.parameters(), None,
+                                                   as_tensor=self.capturable)
+            self.scaler.step(self.optim_d)
+
+        # as in step(): D's weight gradients of the generator pass are
+        # discarded by the next optim_d.zero_grad(), so they are not computed;
+        # the real branch then needs no autograd graph at all
+        d_params = [p for p in self.net_d.parameters() if p.requires_grad]
+        for p in d_params:
+            p.requires_grad_(False)
+        d_ctx = self.net_d.no_sync() if isinstance(self.net_d, DDP) else contextlib.nullcontext()
+        with self.autocast(), d_ctx:
+            with rf("step:D.forward(gen)"):
+                y_d_hat_r, y_d_hat_g, fmap_r, fmap_g = self.net_d(y, y_hat)
+            with rf("step:G.losses"), self.autocast(False):
+                loss_dur = torch.sum(l_length.float()) * hps.train.c_dur
+                loss_mel = torch.nn.functional.l1_loss(y_mel, y_hat_mel) * hps.train.c_mel
+                loss_kl = kl_loss(z_p, logs_q, m_p, logs_p, z_mask) * hps.train.c_kl
+                loss_kl_q = kl_loss(z_q, logs_p, m_q, logs_q, z_mask) * hps.train.c_kl_q
+                loss_fm = feature_loss(fmap_r, fmap_g)
+                loss_gen, _ = generator_loss(y_d_hat_g)
+                loss_gen_all = loss_gen + loss_fm + loss_mel + loss_dur + loss_kl + loss_kl_q
+        with rf("step:G.backward"):
+            self.optim_g.zero_grad()
+            self.scaler.scale(loss_gen_all).backward()
+            if self.allreduce:
+                self._allreduce_grads("g", self.net_g)
+        for p in d_params:
+            p.requires_grad_(True)
+        with rf("step:G.optimizer"):
+            self.scaler.unscale_(self.optim_g)
+            grad_norm_g = commons.clip_grad_value_(self.net_g.parameters(), None,
+                                                   as_tensor=self.capturable)
+            self.scaler.step(self.optim_g)
+            self.scaler.update()
+        return {"loss_disc": loss_disc.detach(), "loss_gen_all": loss_gen_all.detach(),
+                "loss_mel": loss_mel.detach(), "loss_fm": loss_fm.detach(),
+                "loss_dur": loss_dur.detach(), "loss_kl": loss_kl.detach(),
+                "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
 
     def _allreduce_grads(self, key, net):
         """Average this network's gradients over the ranks: one flat buffer,
@@ -301,6 +395,8 @@ def main(argv=None):
     ap.add_argument("-c", "--config", default=None)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--variant", choices=["stft", "mel"], default="stft",
+                    help="stft: train_stft.py (MWSD + MR-STFT); mel: train.py (MPD + mel-L1)")
     args = ap.parse_args(argv)
     hps = utils.get_hparams_from_file(args.config) if args.config else default_hps()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -311,8 +407,8 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank)
     torch.manual_seed(hps.train.seed)
-    net_g, net_d = build_models(hps, device)
-    stepper = TrainStep(hps, net_g, net_d, device, ddp=world > 1)
+    net_g, net_d = build_models(hps, device, args.variant)
+    stepper = TrainStep(hps, net_g, net_d, device, ddp=world > 1, variant=args.variant)
     bs = args.batch or hps.train.batch_size
     batch = synthetic_batch(hps, bs, seed=rank)
     for i in range(args.steps):
