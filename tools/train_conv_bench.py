@@ -65,11 +65,22 @@ def main():
                 y = F.conv1d(xa, w, b, padding=pad, dilation=dil)
             y.backward(dy16)
 
+        def wg():
+            train_ops.wgrad(dy, x.detach(), k, dil, pad, slope)
+
+        def fwd():
+            train_ops.Conv1dHip.apply(x.detach(), w.detach(), b.detach(), dil, pad, slope,
+                                      train_ops.TRAIN_WDTYPE)
+
         th = timeit(hip)
         tr = timeit(ref)
+        tw = timeit(wg)
+        tf = timeit(fwd)
         rows.append(dict(shape=name, hip_ms=round(th, 4), miopen_ms=round(tr, 4),
                          hip_tflops=round(flops / th / 1e9, 1),
-                         miopen_tflops=round(flops / tr / 1e9, 1)))
+                         miopen_tflops=round(flops / tr / 1e9, 1),
+                         wgrad_ms=round(tw, 4), wgrad_tflops=round(flops / 3 / tw / 1e9, 1),
+                         fwd_ms=round(tf, 4), fwd_tflops=round(flops / 3 / tf / 1e9, 1)))
         print(json.dumps(rows[-1]), flush=True)
 
 
