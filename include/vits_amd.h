@@ -312,12 +312,22 @@ typedef struct vits_conv1d_wgrad_desc {
   float* dw_t;            /* += dW as [k][cout][cin] fp32 (caller zeroes)    */
   float* dbias;           /* += sum_{b,t} dY [cout] fp32, or NULL            */
   int32_t wdtype;         /* MFMA operand type: VITS_WDT_F16 / VITS_WDT_BF16 */
-  int32_t reserved;
+  int32_t reserved;       /* > 0: (b, t)-chunks of 64 steps per workgroup    */
+                          /* (tuning override), 0 = automatic                */
 } vits_conv1d_wgrad_desc;
 /* dW[co][ci][j] = sum_{b,t} dY[b][co][t] * act(x[b][ci][t - pad_left + j*dil]) */
 /* (operands rounded to wdtype, fp32 accumulation; VITS_E_UNSUP when       */
 /* 64 + (k-1)*dil > 128 or k not in {1,2,3,4,5,7,9,11})                  */
 int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, void* stream);
+/* Same weight gradient without atomics (deterministic): every (b, t)-split */
+/* workgroup stores its partial tile into `workspace`, a second launch sums */
+/* the splits and WRITES d->dw_t in the parameter layout [cout][cin][k]    */
+/* and d->dbias [cout] (no zeroing needed).  workspace_floats >=           */
+/* vits_conv1d_wgrad_workspace(d, batch).  Replaces the weight-gradient    */
+/* half of torch's conv backward under autocast (train_stft.py:206,232).   */
+int64_t vits_conv1d_wgrad_workspace(const vits_conv1d_wgrad_desc* d, int batch);
+int vits_conv1d_wgrad_split(const vits_conv1d_wgrad_desc* d, int batch, float* workspace,
+                            int64_t workspace_floats, void* stream);
 
 /* WaveNet gate of WN (modules.py:139-146) / ResBlock2 (modules.py:253-255) */
 /* in training: y[b][p][t] = tanh(x[b][p][t] + g[b][p]) *                 */

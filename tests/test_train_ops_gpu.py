@@ -172,3 +172,26 @@ def test_gate_fwd_bwd(device, B, H, T, with_g):
     _close(xd.grad, xr.grad, "dx", tol=1e-5)
     if with_g:
         _close(gd.grad, gr.grad, "dg", tol=1e-5)
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("B,cin,cout,k,dil,pad,T,slope", [
+    (2, 256, 512, 5, 1, 2, 500, 1.0),      # large weight (atomic by default)
+    (3, 32, 32, 7, 3, 9, 1500, 0.1),       # small weight (split by default)
+    (5, 1024, 1, 3, 1, 1, 11, 1.0),        # MPD conv_post: one output row, T < 64
+    (4, 64, 64, 5, 9, 0, 4097, 0.2),       # many (b, t) chunks, odd length
+])
+def test_wgrad_atomic_and_split_modes(device, B, cin, cout, k, dil, pad, T, slope, split):
+    """Both weight-gradient modes (fp32 atomics into [k][cout][cin]; split-K
+    partial tiles + reduce written in [cout][cin][k]) against torch fp32 on
+    the same fp16-rounded operands."""
+    g = torch.Generator().manual_seed(cin * 17 + cout + k + T)
+    x = torch.randn(B, cin, T, generator=g)
+    T_out = T + 2 * pad - (k - 1) * dil
+    dy = torch.randn(B, cout, T_out, generator=g)
+    dw, db = train_ops.wgrad(dy.to(device), x.to(device), k, dil, pad, slope, split=split)
+    xr = _r16(F.leaky_relu(x, slope) if slope != 1.0 else x)
+    wr = torch.zeros(cout, cin, k, requires_grad=True)
+    F.conv1d(xr, wr, None, padding=pad, dilation=dil).backward(_r16(dy))
+    _close(dw, wr.grad, "dw")
+    _close(db, dy.sum((0, 2)), "db")

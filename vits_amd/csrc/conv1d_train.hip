@@ -71,10 +71,16 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)ua | ((uint32_t)ub << 16);
 }
 
-template <int NK, int WT>
+// PARTIAL: each (b, t)-split workgroup stores its partial tile with plain
+// stores into ws[split][k][cout][cin] (+ bias partials ws_b[split][cout]);
+// wgrad_reduce_kernel then sums the splits.  Otherwise fp32 atomics into
+// p.dw_t / p.dbias.
+template <int NK, int WT, bool PARTIAL>
 __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_conv1d_wgrad_desc p,
                                                                      int tchunks, int total_chunks,
-                                                                     int chunks_per_wg) {
+                                                                     int chunks_per_wg,
+                                                                     float* __restrict__ ws,
+                                                                     float* __restrict__ ws_b) {
   typedef typename Op16<WT>::V8 V8;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   const int tid = threadIdx.x;
@@ -211,15 +217,21 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
     __syncthreads();
   }
 
-  // ---- epilogue: fp32 atomics into dw_t[j][co][ci] ---------------------------
+  // ---- epilogue: dw_t[j][co][ci] (atomics) or the split's partial tile ------
   const int ci = c0 + wn + l32;
+  float* dst = PARTIAL ? ws + (int64_t)blockIdx.x * NK * p.cout * p.cin : p.dw_t;
 #pragma unroll
   for (int j = 0; j < NK; ++j) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = m0 + wm + 8 * (r >> 2) + 4 * lhi + (r & 3);
-      if (co < p.cout && ci < p.cin)
-        unsafeAtomicAdd(p.dw_t + ((int64_t)j * p.cout + co) * p.cin + ci, acc[j][r]);
+      if (co < p.cout && ci < p.cin) {
+        float* a = dst + ((int64_t)j * p.cout + co) * p.cin + ci;
+        if constexpr (PARTIAL)
+          *a = acc[j][r];
+        else
+          unsafeAtomicAdd(a, acc[j][r]);
+      }
     }
   }
   if (do_bias) {
@@ -229,28 +241,110 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
       const int co = m0 + dy_row0 + 8 * q;
-      if ((tid & 31) == 0 && co < p.cout) unsafeAtomicAdd(p.dbias + co, v);
+      if ((tid & 31) == 0 && co < p.cout) {
+        if constexpr (PARTIAL)
+          ws_b[(int64_t)blockIdx.x * p.cout + co] = v;
+        else
+          unsafeAtomicAdd(p.dbias + co, v);
+      }
     }
   }
 }
 
-template <int WT>
-int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s) {
-  const int tchunks = (d.n_out + KT - 1) / KT;
-  const int total = batch * tchunks;
+// dw[co][ci][j] = sum_s ws[s][j][co][ci] (the parameter layout, written, not
+// accumulated: no zeroing), dbias[co] = sum_s ws_b[s][co].  A workgroup
+// reduces E = 256 / P consecutive slab elements with P lanes each over the
+// splits (coalesced reads along the slab, <= ~16 loads per thread), then
+// combines the P partial sums in LDS.  Blocks past the slab's do the bias.
+template <int P>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws,
+                                                           const float* __restrict__ ws_b,
+                                                           int splits, int k, int cout, int cin,
+                                                           int slab_blocks, float* __restrict__ dw,
+                                                           float* __restrict__ dbias) {
+  constexpr int E = 256 / P;
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  const int el = tid % E;
+  const int q = tid / E;
+  const int64_t n = (int64_t)cout * cin;
+  const bool bias_blk = (int)blockIdx.x >= slab_blocks;
+  const int64_t total = bias_blk ? cout : n * k;
+  const float* src = bias_blk ? ws_b : ws;
+  const int64_t e = (int64_t)(bias_blk ? blockIdx.x - slab_blocks : blockIdx.x) * E + el;
+  float a0 = 0.f, a1 = 0.f;
+  if (e < total) {
+    int s = q;
+    for (; s + P < splits; s += 2 * P) {
+      a0 += src[(int64_t)s * total + e];
+      a1 += src[(int64_t)(s + P) * total + e];
+    }
+    if (s < splits) a0 += src[(int64_t)s * total + e];
+  }
+  red[tid] = a0 + a1;
+  __syncthreads();
+#pragma unroll
+  for (int off = P / 2; off > 0; off >>= 1) {
+    if (q < off) red[tid] += red[tid + off * E];
+    __syncthreads();
+  }
+  if (q == 0 && e < total) {
+    if (bias_blk) {
+      dbias[e] = red[tid];
+    } else {
+      const int64_t j = e / n;
+      const int64_t i = e - j * n;
+      dw[i * k + j] = red[tid];
+    }
+  }
+}
+
+// (b, t)-chunks per workgroup.  Atomic mode: >= 16 chunks (1024 time steps)
+// per workgroup (512 FLOP per atomic byte), beyond that about 1024
+// workgroups.  Split mode: about 2048 workgroups, >= 4 chunks each, and the
+// partial tiles (splits x k x cout x cin floats) capped near 2x the work's
+// own input bytes so the workspace pass stays small next to the MFMA work.
+struct WgradSplit {
+  int tchunks, total, cpw, splits;
+};
+WgradSplit wgrad_split(const vits_conv1d_wgrad_desc& d, int batch, bool partial) {
+  WgradSplit w;
+  w.tchunks = (d.n_out + KT - 1) / KT;
+  w.total = batch * w.tchunks;
   const int tiles = ((d.cout + WG_M - 1) / WG_M) * ((d.cin + WG_N - 1) / WG_N);
-  // >= 16 chunks (1024 time steps) per workgroup: 512 FLOP per atomic byte;
-  // beyond that, about 1024 workgroups
-  int cpw = (int)(((int64_t)total * tiles + 1023) / 1024);
-  const int min_cpw = total < 16 ? total : 16;
-  if (cpw < min_cpw) cpw = min_cpw;
-  const int splits = (total + cpw - 1) / cpw;
-  dim3 grid(splits, (d.cin + WG_N - 1) / WG_N, (d.cout + WG_M - 1) / WG_M);
+  if (!partial) {
+    w.cpw = (int)(((int64_t)w.total * tiles + 1023) / 1024);
+    const int min_cpw = w.total < 16 ? w.total : 16;
+    if (w.cpw < min_cpw) w.cpw = min_cpw;
+  } else {
+    // 16 chunks per workgroup (measured best on the training shapes,
+    // tools/wgrad_split_bench.py: faster than the atomic mode on every one,
+    // 92.8 -> 76 us enc_q WN, 127.6 -> 81.5 us MWD scale 0), then at most
+    // ~2048 workgroups
+    w.cpw = (int)(((int64_t)w.total * tiles + 2047) / 2048);
+    const int min_cpw = w.total < 16 ? w.total : 16;
+    if (w.cpw < min_cpw) w.cpw = min_cpw;
+    // fewer than one workgroup per CU: halve the chunks per workgroup
+    // (the MWD scale-4 shape: 60 -> 43 us)
+    if (w.cpw == 16 && (int64_t)((w.total + 15) / 16) * tiles < 256) w.cpw = 8;
+  }
+  if (d.reserved > 0) w.cpw = d.reserved < w.total ? d.reserved : w.total;  // explicit override
+  w.splits = (w.total + w.cpw - 1) / w.cpw;
+  return w;
+}
+
+template <int WT, bool PARTIAL>
+int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, float* ws,
+                   float* ws_b) {
+  const WgradSplit w = wgrad_split(d, batch, PARTIAL);
+  const int tchunks = w.tchunks, total = w.total, cpw = w.cpw;
+  dim3 grid(w.splits, (d.cin + WG_N - 1) / WG_N, (d.cout + WG_M - 1) / WG_M);
   const size_t lds = 2 * STAGE_HALVES * sizeof(uint16_t);
   switch (d.k) {
 #define VITS_WG_CASE(NK) \
   case NK:               \
-    hipLaunchKernelGGL((wgrad_kernel<NK, WT>), grid, dim3(256), lds, s, d, tchunks, total, cpw); \
+    hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL>), grid, dim3(256), lds, s, d, tchunks, total, \
+                       cpw, ws, ws_b);                                                            \
     break;
     VITS_WG_CASE(1)
     VITS_WG_CASE(2)
@@ -307,9 +401,61 @@ extern "C" int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, voi
   VITS_CHECK_ARG(batch > 0 && d->cout > 0 && d->cin > 0 && d->k > 0 && d->dil > 0);
   VITS_CHECK_SHAPE(d->n_out > 0 && d->tin > 0);
   if (KT + (d->k - 1) * d->dil > MAX_WR) return VITS_E_UNSUP;
-  if (d->wdtype == VITS_WDT_F16) return wgrad_dispatch<VITS_WDT_F16>(*d, batch, as_stream(stream));
-  if (d->wdtype == VITS_WDT_BF16) return wgrad_dispatch<VITS_WDT_BF16>(*d, batch, as_stream(stream));
+  hipStream_t s = as_stream(stream);
+  if (d->wdtype == VITS_WDT_F16) return wgrad_dispatch<VITS_WDT_F16, false>(*d, batch, s, 0, 0);
+  if (d->wdtype == VITS_WDT_BF16) return wgrad_dispatch<VITS_WDT_BF16, false>(*d, batch, s, 0, 0);
   return VITS_E_ARG;
+}
+
+extern "C" int64_t vits_conv1d_wgrad_workspace(const vits_conv1d_wgrad_desc* d, int batch) {
+  if (!d || batch <= 0 || d->cout <= 0 || d->cin <= 0 || d->k <= 0 || d->n_out <= 0) return 0;
+  const WgradSplit w = wgrad_split(*d, batch, true);
+  return (int64_t)w.splits * ((int64_t)d->k * d->cout * d->cin + d->cout);
+}
+
+extern "C" int vits_conv1d_wgrad_split(const vits_conv1d_wgrad_desc* d, int batch, float* workspace,
+                                       int64_t workspace_floats, void* stream) {
+  if (!d) return VITS_E_ARG;
+  VITS_CHECK_ARG(d->dy && d->x && d->dw_t && workspace);
+  VITS_CHECK_ARG(batch > 0 && d->cout > 0 && d->cin > 0 && d->k > 0 && d->dil > 0);
+  VITS_CHECK_SHAPE(d->n_out > 0 && d->tin > 0);
+  if (KT + (d->k - 1) * d->dil > MAX_WR) return VITS_E_UNSUP;
+  if (workspace_floats < vits_conv1d_wgrad_workspace(d, batch)) return VITS_E_ARG;
+  const WgradSplit w = wgrad_split(*d, batch, true);
+  float* ws_b = workspace + (int64_t)w.splits * d->k * d->cout * d->cin;
+  hipStream_t s = as_stream(stream);
+  int rc;
+  if (d->wdtype == VITS_WDT_F16)
+    rc = wgrad_dispatch<VITS_WDT_F16, true>(*d, batch, s, workspace, ws_b);
+  else if (d->wdtype == VITS_WDT_BF16)
+    rc = wgrad_dispatch<VITS_WDT_BF16, true>(*d, batch, s, workspace, ws_b);
+  else
+    return VITS_E_ARG;
+  if (rc) return rc;
+  // split-lanes per element: enough that each thread sums <= ~16 splits
+  int P = 1;
+  while (P < 64 && P * 16 < w.splits) P *= 2;
+  const int E = 256 / P;
+  const int64_t slab = (int64_t)d->k * d->cout * d->cin;
+  const int slab_blocks = (int)((slab + E - 1) / E);
+  const int bias_blocks = d->dbias ? (d->cout + E - 1) / E : 0;
+  const dim3 grid(slab_blocks + bias_blocks);
+  switch (P) {
+#define VITS_RED_CASE(PP)                                                                          \
+  case PP:                                                                                         \
+    hipLaunchKernelGGL(wgrad_reduce_kernel<PP>, grid, dim3(256), 0, s, workspace, ws_b, w.splits, \
+                       d->k, d->cout, d->cin, slab_blocks, d->dw_t, d->dbias);                    \
+    break;
+    VITS_RED_CASE(1)
+    VITS_RED_CASE(2)
+    VITS_RED_CASE(4)
+    VITS_RED_CASE(8)
+    VITS_RED_CASE(16)
+    VITS_RED_CASE(32)
+    VITS_RED_CASE(64)
+#undef VITS_RED_CASE
+  }
+  return vits_launch_status();
 }
 
 extern "C" int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, void* out,

@@ -10,6 +10,8 @@ MultiWaveSTFTDiscriminator 200-236.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -195,6 +197,13 @@ class MultiWaveSTFTDiscriminator(nn.Module):
 # ---------------------------------------------------------------------------
 
 MPD_LRELU_SLOPE = 0.1  # modules.LRELU_SLOPE (models.py:347,374)
+_MPD_HIP = os.environ.get("VITS_MPD_HIP", "1") != "0"  # diagnostics switch
+
+
+def _hip_wdtype(x):
+    if not _MPD_HIP or x.device.type != "cuda":
+        return None
+    return train_ops.autocast_wdtype(x.device.type)
 
 
 def _wn_weight(m: nn.Module) -> torch.Tensor:
@@ -249,18 +258,15 @@ class DiscriminatorP(nn.Module):
         for layer in self.convs:
             w = _wn_weight(layer).squeeze(-1)
             s, pd = layer.stride[0], layer.padding[0]
-            if s == 1 and train_ops.autocast_wdtype(x.device.type) is not None \
-                    and x.device.type == "cuda":
-                x = train_ops.Conv1dHip.apply(x, w, layer.bias, 1, pd, 1.0,
-                                              train_ops.autocast_wdtype(x.device.type))
+            if s == 1 and _hip_wdtype(x) is not None:
+                x = train_ops.Conv1dHip.apply(x, w, layer.bias, 1, pd, 1.0, _hip_wdtype(x))
             else:
                 x = F.conv1d(x, w, layer.bias, stride=s, padding=pd)
             x = F.leaky_relu(x, MPD_LRELU_SLOPE)
             fmap.append(x.view(b, p, x.shape[1], x.shape[2]).permute(0, 2, 3, 1))
         w = _wn_weight(self.conv_post).squeeze(-1)
-        if train_ops.autocast_wdtype(x.device.type) is not None and x.device.type == "cuda":
-            x = train_ops.Conv1dHip.apply(x, w, self.conv_post.bias, 1, 1, 1.0,
-                                          train_ops.autocast_wdtype(x.device.type))
+        if _hip_wdtype(x) is not None:
+            x = train_ops.Conv1dHip.apply(x, w, self.conv_post.bias, 1, 1, 1.0, _hip_wdtype(x))
         else:
             x = F.conv1d(x, w, self.conv_post.bias, padding=1)
         x = x.view(b, p, 1, x.shape[2]).permute(0, 2, 3, 1)
@@ -300,7 +306,7 @@ class DiscriminatorS(nn.Module):
         self.conv_post = norm_f(Conv1d(1024, 1, 3, 1, padding=1))
 
     def _conv(self, layer, x):
-        if not self.use_spectral_norm:
+        if not self.use_spectral_norm and _MPD_HIP:
             return train_ops.conv1d(layer, x)  # HIP when supported + autocast, else torch
         return layer(x)
 

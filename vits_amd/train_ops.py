@@ -81,30 +81,62 @@ def wgrad_buffer(cout: int, cin: int, k: int, with_bias: bool, device, zeroed: b
     return alloc(n, device=device, dtype=torch.float32)
 
 
+def use_split_wgrad(cout: int, cin: int, k: int) -> bool:
+    """Split-K weight gradient (partial tiles + one reduce launch, no atomics,
+    deterministic, written straight into the parameter layout): faster than
+    the atomic mode on every training shape measured with
+    tools/wgrad_split_bench.py (8-36 %), so it is the default; the atomic
+    mode stays for callers that accumulate into a buffer."""
+    return k * cout * cin <= SPLIT_WGRAD_MAX
+
+
+SPLIT_WGRAD_MAX = 1 << 40
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, k: int, dil: int, pad_left: int,
           in_slope: float = 1.0, with_bias: bool = True, wdtype: int = TRAIN_WDTYPE,
-          buf: torch.Tensor | None = None):
+          buf: torch.Tensor | None = None, split: bool | None = None):
     """dW [Cout, Cin, k] and dbias [Cout] (fp32) of y = conv1d(act(x), W) + b.
-    ``buf``: a zeroed wgrad_buffer (else one is allocated)."""
+    ``buf``: a zeroed wgrad_buffer (atomic mode; else one is allocated).
+    ``split``: split-K mode (default: ``use_split_wgrad``)."""
     B, cout, n_out = dy.shape
     _, cin, tin = x.shape
     assert dy.stride(2) == 1 and x.stride(2) == 1 and dy.dtype == x.dtype == torch.float32
+    if split is None:
+        split = buf is None and use_split_wgrad(cout, cin, k)
+    if split:
+        dw = torch.empty(cout, cin, k, device=dy.device, dtype=torch.float32)
+        db = torch.empty(cout, device=dy.device, dtype=torch.float32) if with_bias else None
+        d = _wgrad_desc(dy, x, k, dil, pad_left, in_slope, dw, db, wdtype)
+        lib = _lib.load()
+        nws = int(lib.vits_conv1d_wgrad_workspace(d, B))
+        ws = torch.empty(max(nws, 1), device=dy.device, dtype=torch.float32)
+        check(lib.vits_conv1d_wgrad_split(d, B, ws.data_ptr(), nws, _stream_ptr(dy.device)),
+              "vits_conv1d_wgrad_split")
+        return dw, db
     if buf is None:
         buf = wgrad_buffer(cout, cin, k, with_bias, dy.device)
     dw_t = buf[:k * cout * cin].view(k, cout, cin)
     db = buf[k * cout * cin:] if with_bias else None
+    d = _wgrad_desc(dy, x, k, dil, pad_left, in_slope, dw_t, db, wdtype)
+    check(_lib.load().vits_conv1d_wgrad(d, B, _stream_ptr(dy.device)), "vits_conv1d_wgrad")
+    if k == 1:  # [1][cout][cin] is already the parameter layout
+        return dw_t.view(cout, cin, 1), db
+    return dw_t.permute(1, 2, 0).contiguous(), db
+
+
+def _wgrad_desc(dy, x, k, dil, pad_left, in_slope, dw, db, wdtype):
+    cout, n_out = dy.shape[1], dy.shape[2]
+    cin, tin = x.shape[1], x.shape[2]
     d = ConvWgradDesc()
     d.dy, d.dy_bstride, d.dy_cstride, d.cout = dy.data_ptr(), dy.stride(0), dy.stride(1), cout
     d.x, d.x_bstride, d.x_cstride, d.cin = x.data_ptr(), x.stride(0), x.stride(1), cin
     d.tin, d.n_out, d.k, d.dil, d.pad_left = tin, n_out, k, dil, pad_left
     d.in_slope = in_slope
-    d.dw_t = dw_t.data_ptr()
+    d.dw_t = dw.data_ptr()
     d.dbias = None if db is None else db.data_ptr()
     d.wdtype = wdtype
-    check(_lib.load().vits_conv1d_wgrad(d, B, _stream_ptr(dy.device)), "vits_conv1d_wgrad")
-    if k == 1:  # [1][cout][cin] is already the parameter layout
-        return dw_t.view(cout, cin, 1), db
-    return dw_t.permute(1, 2, 0).contiguous(), db
+    return d
 
 
 class Conv1dHip(torch.autograd.Function):
@@ -135,15 +167,17 @@ class Conv1dHip(torch.autograd.Function):
         dx = dw = db = buf = None
         cout, cin = w32.shape[0], w32.shape[1]
         want_w = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
+        split = use_split_wgrad(cout, cin, k)
         if ctx.needs_input_grad[0]:
-            # the weight-gradient accumulator is cleared by the packing launch
-            if want_w:
+            # the atomic weight-gradient accumulator is cleared by the packing launch
+            if want_w and not split:
                 buf = wgrad_buffer(cout, cin, k, has_bias, dy.device, zeroed=False)
             layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, zero=buf)
             dx = _run(dy, layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
                       gmask_slope=slope)
         if want_w:
-            dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype, buf=buf)
+            dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype, buf=buf,
+                           split=split)
         return dx, dw, db, None, None, None, None
 
 
