@@ -176,6 +176,32 @@ def _event_ms(fn, reps=20, warmup=3):
     return s.elapsed_time(e) / reps
 
 
+def _graph_ms(fn, reps=20, warmup=3):
+    """Device time per call of ``fn``: ``reps`` calls captured into one
+    hipGraph and replayed, timed with events on the replay stream, so host
+    launch overhead (the Python wrapper: ~20-60 us per call) is excluded --
+    these small kernels are shorter than their host-side call."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(warmup):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(reps):
+            fn()
+    graph.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    graph.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
 def latency_leg(model, device, reps=10):
     """Serving latency (EmoVITS / VITSWrap call pattern, one utterance):
     infer_p1 (text encoder + duration predictor) + infer_p2 (flow + decoder)
@@ -218,7 +244,9 @@ def kernels_leg(device):
     """The training-side HIP kernels at BASELINE C3 shapes (B=64, t_t=500
     frames, t_s=100 tokens, 9216-sample segments), each against its roofline
     (SURVEY §8(d)): MAS (latency-bound DP; HBM fraction reported), MR-STFT
-    magnitudes (HBM), neg_cent (fp32 MFMA)."""
+    magnitudes (HBM), neg_cent (fp32 MFMA).  Device time per call from
+    hipGraph replays (_graph_ms); the loss fwd+bwd is the eager host-side
+    call."""
     from vits_amd import ops
     from vits_amd.stft_loss import MultiResolutionSTFTLoss
 
@@ -227,12 +255,12 @@ def kernels_leg(device):
     nc = torch.randn(B, Tt, Ts, generator=g).to(device)
     tt = torch.full((B,), Tt, dtype=torch.int32, device=device)
     ts = torch.full((B,), Ts, dtype=torch.int32, device=device)
-    mas_ms = _event_ms(lambda: ops.maximum_path_lengths(nc, tt, ts))
+    mas_ms = _graph_ms(lambda: ops.maximum_path_lengths(nc, tt, ts))
     mas_bytes = B * Tt * Ts * 8
     z = torch.randn(B, C, Tt, generator=g).to(device)
     m = torch.randn(B, C, Ts, generator=g).to(device)
     lg = (torch.randn(B, C, Ts, generator=g) * 0.5).to(device)
-    nc_ms = _event_ms(lambda: ops.neg_cent(z, m, lg))
+    nc_ms = _graph_ms(lambda: ops.neg_cent(z, m, lg))
     nc_flops = 2 * 2 * C * Tt * Ts * B
     loss = MultiResolutionSTFTLoss().to(device)
     y = (torch.randn(B, L, generator=g) * 0.1).to(device)
@@ -240,7 +268,7 @@ def kernels_leg(device):
     specs = [(f.window, f.fft_size, f.hop_size, f.win_size, None, 1e-7) for f in loss.stft_losses]
     yd = yh.detach()
     # the loss's forward: both signals x 5 resolutions in one launch
-    fwd_ms = _event_ms(lambda: ops.stft_mag_multi([y] * 5 + [yd] * 5, specs + specs))
+    fwd_ms = _graph_ms(lambda: ops.stft_mag_multi([y] * 5 + [yd] * 5, specs + specs))
     mags = sum((f.fft_size // 2 + 1) * (L // f.hop_size + 1) for f in loss.stft_losses)
     fwd_bytes = 2 * B * (len(loss.stft_losses) * L * 4 + mags * 4)
 

@@ -68,6 +68,130 @@ __global__ __launch_bounds__(64) void neg_cent_kernel(const float* __restrict__ 
   }
 }
 
+// v2: one workgroup = one 32-column x tile of one utterance and 8 y tiles
+// (two per wave, y0 and y0 + 128, as two independent accumulator chains).  The B operand of every d (s = exp(-2 logs), m s) and the
+// per-column constant are computed ONCE per workgroup into LDS (v1 recomputed
+// them in each of the t_t/32 waves of a column tile, exp included), and each
+// wave prefetches its z_p rows 8 channel pairs ahead of the MFMAs, so the
+// kernel runs at the MFMA rate instead of the load latency.
+constexpr int NC_PF = 8;  // channel pairs per prefetch group
+
+__global__ __launch_bounds__(256) void neg_cent_kernel2(const float* __restrict__ z,
+                                                        const float* __restrict__ m,
+                                                        const float* __restrict__ logs,
+                                                        float* __restrict__ out, int C, int Tt,
+                                                        int Ts) {
+  extern __shared__ float lds[];
+  float* sS = lds;                 // [C][32]   s
+  float* sMS = lds + C * 32;       // [C][32]   m s
+  float* cpart = sMS + C * 32;     // [8][32]   per-column constant partials
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int l32 = lane & 31;
+  const int lhi = lane >> 5;
+  const int x0 = blockIdx.x * 32;
+  const int b = blockIdx.z;
+  const float* mb = m + (int64_t)b * C * Ts;
+  const float* lb = logs + (int64_t)b * C * Ts;
+  constexpr float kHalfLog2Pi = 0.918938533204672742f;  // 0.5 * log(2 pi)
+  {
+    const int xl = tid & 31;
+    const int x = x0 + xl;
+    float cp = 0.f;
+    // 8 rows (d) per thread in flight at once: the loads of a group are all
+    // issued before the first is used (a load-use chain per row would
+    // serialise ~C/8 global latencies)
+    constexpr int G = 8;
+    for (int d0 = tid >> 5; d0 < C; d0 += 8 * G) {
+      float lv[G], mv[G];
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int d = d0 + 8 * i;
+        const bool ok = d < C && x < Ts;
+        lv[i] = ok ? lb[(int64_t)d * Ts + x] : 0.f;
+        mv[i] = ok ? mb[(int64_t)d * Ts + x] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int d = d0 + 8 * i;
+        if (d < C) {
+          float sv = 0.f, msv = 0.f;
+          if (x < Ts) {
+            sv = expf(-2.0f * lv[i]);
+            msv = mv[i] * sv;
+            cp += -kHalfLog2Pi - lv[i] - 0.5f * (mv[i] * mv[i]) * sv;
+          }
+          sS[d * 32 + xl] = sv;
+          sMS[d * 32 + xl] = msv;
+        }
+      }
+    }
+    cpart[tid] = cp;
+  }
+  __syncthreads();
+  // two y tiles per wave (rows y0 and y0 + 128): two independent MFMA
+  // accumulator chains sharing every B-operand LDS read
+  const int y0 = (blockIdx.y * 8 + wid) * 32;
+  if (y0 >= Tt) return;
+  float colc = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) colc += cpart[q * 32 + l32];
+  const int ya = y0 + l32;
+  const int yb = ya + 128;
+  const bool yva = ya < Tt;
+  const bool yvb = yb < Tt;
+  const float* zb = z + (int64_t)b * C * Tt;
+  const float* za = zb + (yva ? ya : 0);
+  const float* zbb = zb + (yvb ? yb : 0);
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = 0.f;
+    acc1[r] = 0.f;
+  }
+  const int pairs = (C + 1) >> 1;
+  float zna[NC_PF], znb[NC_PF];
+  auto zload = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < NC_PF; ++i) {
+      const int d = 2 * (p0 + i) + lhi;
+      zna[i] = (yva && d < C) ? za[(int64_t)d * Tt] : 0.f;
+      znb[i] = (yvb && d < C) ? zbb[(int64_t)d * Tt] : 0.f;
+    }
+  };
+  zload(0);
+  for (int p0 = 0; p0 < pairs; p0 += NC_PF) {
+    float zca[NC_PF], zcb[NC_PF];
+#pragma unroll
+    for (int i = 0; i < NC_PF; ++i) {
+      zca[i] = zna[i];
+      zcb[i] = znb[i];
+    }
+    if (p0 + NC_PF < pairs) zload(p0 + NC_PF);
+#pragma unroll
+    for (int i = 0; i < NC_PF; ++i) {
+      const int d = 2 * (p0 + i) + lhi;
+      const bool dv = d < C;
+      const float sv = dv ? sS[d * 32 + l32] : 0.f;
+      const float msv = dv ? sMS[d * 32 + l32] : 0.f;
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(-0.5f * zca[i] * zca[i], sv, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(-0.5f * zcb[i] * zcb[i], sv, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(zca[i], msv, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(zcb[i], msv, acc1, 0, 0, 0);
+    }
+  }
+  const int x = x0 + l32;
+  if (x >= Ts) return;
+  float* ob = out + (int64_t)b * Tt * Ts;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = y0 + (r & 3) + 8 * (r >> 2) + 4 * lhi;
+    if (row < Tt) ob[(int64_t)row * Ts + x] = acc0[r] + colc;
+    if (row + 128 < Tt) ob[(int64_t)(row + 128) * Ts + x] = acc1[r] + colc;
+  }
+}
+
 }  // namespace
 
 extern "C" int vits_neg_cent(const float* z_p, const float* m_p, const float* logs_p,
@@ -75,8 +199,15 @@ extern "C" int vits_neg_cent(const float* z_p, const float* m_p, const float* lo
                              void* stream) {
   VITS_CHECK_ARG(z_p && m_p && logs_p && neg_cent);
   VITS_CHECK_ARG(batch > 0 && channels > 0 && t_t > 0 && t_s > 0);
-  dim3 grid((t_s + 31) / 32, (t_t + 31) / 32, batch);
-  hipLaunchKernelGGL(neg_cent_kernel, grid, dim3(64), 0, as_stream(stream), z_p, m_p, logs_p,
-                     neg_cent, channels, t_t, t_s);
+  const size_t lds = sizeof(float) * (2 * (size_t)channels * 32 + 256);
+  if (lds <= 64 * 1024) {
+    dim3 grid((t_s + 31) / 32, (t_t + 255) / 256, batch);
+    hipLaunchKernelGGL(neg_cent_kernel2, grid, dim3(256), lds, as_stream(stream), z_p, m_p, logs_p,
+                       neg_cent, channels, t_t, t_s);
+  } else {  // very wide channel counts: the LDS-free v1
+    dim3 grid((t_s + 31) / 32, (t_t + 31) / 32, batch);
+    hipLaunchKernelGGL(neg_cent_kernel, grid, dim3(64), 0, as_stream(stream), z_p, m_p, logs_p,
+                       neg_cent, channels, t_t, t_s);
+  }
   return vits_launch_status();
 }
