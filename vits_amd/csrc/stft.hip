@@ -72,6 +72,124 @@ __device__ float2* fft_lds(float2* a, float2* b, const float2* tw, int n, int lo
   return a;
 }
 
+// Compile-time twiddle table: (cos, sin)(2 pi m / FFT_MAX), m < FFT_MAX / 2,
+// from double-precision Taylor series rounded to float (no per-workgroup
+// sincos fill, no LDS for twiddles).  Size-n transforms read it with stride
+// FFT_MAX / n.
+struct TwTable {
+  float c[FFT_MAX / 2];
+  float s[FFT_MAX / 2];
+};
+constexpr double kPi = 3.14159265358979323846264338327950288;
+constexpr double taylor_sin(double x) {
+  double term = x, sum = x;
+  for (int k = 1; k < 24; ++k) {
+    term *= -x * x / ((2.0 * k) * (2.0 * k + 1.0));
+    sum += term;
+  }
+  return sum;
+}
+constexpr double taylor_cos(double x) {
+  double term = 1.0, sum = 1.0;
+  for (int k = 1; k < 24; ++k) {
+    term *= -x * x / ((2.0 * k - 1.0) * (2.0 * k));
+    sum += term;
+  }
+  return sum;
+}
+constexpr TwTable make_tw() {
+  TwTable t{};
+  for (int m = 0; m < FFT_MAX / 2; ++m) {
+    // reduce to [0, pi/2]: theta in [0, pi)
+    const double th = 2.0 * kPi * m / FFT_MAX;
+    const bool hi = th > kPi / 2;
+    const double r = hi ? kPi - th : th;
+    t.c[m] = (float)(hi ? -taylor_cos(r) : taylor_cos(r));
+    t.s[m] = (float)taylor_sin(r);
+  }
+  return t;
+}
+__constant__ TwTable g_tw = make_tw();
+
+// the workgroup's n/2 twiddles of size n, copied from the constant table
+// into LDS (coalesced reads; divergent constant-table reads per butterfly
+// measured slower: 182 -> 231 us)
+__device__ void load_twiddles(float2* tw, int n) {
+  const int stride = FFT_MAX / n;
+  for (int m = threadIdx.x; m < (n >> 1); m += blockDim.x)
+    tw[m] = make_float2(g_tw.c[m * stride], g_tw.s[m * stride]);
+}
+
+// Twiddle e^{sign 2 pi i m / n} for 0 <= m < n (e^{i(t + pi)} = -e^{i t}).
+__device__ __forceinline__ float2 twiddle(const float2* tw, int m, int n, float sign) {
+  const int half = n >> 1;
+  float2 w = tw[m < half ? m : m - half];
+  if (m >= half) w = make_float2(-w.x, -w.y);
+  return make_float2(w.x, sign * w.y);
+}
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+  return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+
+// Mixed radix-4 Stockham (one radix-2 stage first when log2 n is odd): the
+// same autosort formulation as fft_lds with half the stages / barriers /
+// LDS round trips.  Stage with span Ns and radix R, item j < n/R:
+//   v[r] = src[j + r n/R] * e^{sign 2 pi i (j mod Ns) r / (Ns R)}
+//   DFT_R(v) -> dst[(j / Ns) Ns R + (j mod Ns) + r Ns]
+__device__ float2* fft_lds4(float2* a, float2* b, const float2* tw, int n, int log2n, int fpb,
+                            float sign) {
+  int ns = 1;
+  if (log2n & 1) {  // radix-2 stage, Ns = 1: no twiddles
+    const int half = n >> 1;
+    for (int i = threadIdx.x; i < fpb * half; i += blockDim.x) {
+      const int f = i / half;
+      const int j = i - f * half;
+      const float2 v0 = a[f * n + j], v1 = a[f * n + j + half];
+      b[f * n + 2 * j] = make_float2(v0.x + v1.x, v0.y + v1.y);
+      b[f * n + 2 * j + 1] = make_float2(v0.x - v1.x, v0.y - v1.y);
+    }
+    __syncthreads();
+    float2* t = a;
+    a = b;
+    b = t;
+    ns = 2;
+  }
+  const int q = n >> 2;
+  for (; ns < n; ns <<= 2) {
+    const int tstep = n / (ns * 4);  // table index per unit of (j mod Ns) r
+    for (int i = threadIdx.x; i < fpb * q; i += blockDim.x) {
+      const int f = i / q;
+      const int j = i - f * q;
+      const float2* src = a + f * n;
+      float2* dst = b + f * n;
+      const int k = j & (ns - 1);
+      float2 v0 = src[j], v1 = src[j + q], v2 = src[j + 2 * q], v3 = src[j + 3 * q];
+      if (ns > 1) {
+        v1 = cmul(v1, twiddle(tw, k * tstep, n, sign));
+        v2 = cmul(v2, twiddle(tw, 2 * k * tstep, n, sign));
+        v3 = cmul(v3, twiddle(tw, 3 * k * tstep, n, sign));
+      }
+      const float2 t0 = make_float2(v0.x + v2.x, v0.y + v2.y);
+      const float2 t1 = make_float2(v0.x - v2.x, v0.y - v2.y);
+      const float2 t2 = make_float2(v1.x + v3.x, v1.y + v3.y);
+      const float2 d13 = make_float2(v1.x - v3.x, v1.y - v3.y);
+      // t3 = (sign i) (v1 - v3)
+      const float2 t3 = sign < 0.f ? make_float2(d13.y, -d13.x) : make_float2(-d13.y, d13.x);
+      const int o = ((j - k) << 2) + k;
+      dst[o] = make_float2(t0.x + t2.x, t0.y + t2.y);
+      dst[o + ns] = make_float2(t1.x + t3.x, t1.y + t3.y);
+      dst[o + 2 * ns] = make_float2(t0.x - t2.x, t0.y - t2.y);
+      dst[o + 3 * ns] = make_float2(t1.x - t3.x, t1.y - t3.y);
+    }
+    __syncthreads();
+    float2* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
 // One transform job (a signal batch at one resolution), device side.
 struct StftJobD {
   const float* x;       // forward input [B][L]
@@ -86,13 +204,14 @@ struct StftJobD {
   float eps;
 };
 
-// forward: frames f0 .. f0+fpb-1 of utterance b
+// forward: frames f0 .. f0+fpb-1 of utterance b (radix-4 Stockham, fft_lds4;
+// fft_lds is the radix-2 reference formulation it replaced)
 __device__ void stft_fwd_block(const StftJobD& J, int fblk, int b, float2* sfft) {
   const int n = J.n, fpb = J.fpb;
   float2* a = sfft;
   float2* bbuf = sfft + fpb * n;
   float2* tw = bbuf + fpb * n;
-  fill_twiddles(tw, n);
+  load_twiddles(tw, n);
   const int f0 = fblk * fpb;
   const int woff = (n - J.win) / 2;
   const float* xb = J.x + (int64_t)b * J.L;
@@ -109,7 +228,7 @@ __device__ void stft_fwd_block(const StftJobD& J, int fblk, int b, float2* sfft)
     a[i] = make_float2(v, 0.f);
   }
   __syncthreads();
-  const float2* out = fft_lds(a, bbuf, tw, n, J.log2n, fpb, -1.f);
+  const float2* out = fft_lds4(a, bbuf, tw, n, J.log2n, fpb, -1.f);
   const int nb = n / 2 + 1;
   for (int i = threadIdx.x; i < fpb * nb; i += blockDim.x) {
     const int k = i / fpb;
@@ -131,7 +250,7 @@ __device__ void stft_bwd_frames_block(const StftJobD& J, int fblk, int b, float2
   float2* a = sfft;
   float2* bbuf = sfft + fpb * n;
   float2* tw = bbuf + fpb * n;
-  fill_twiddles(tw, n);
+  load_twiddles(tw, n);
   const int f0 = fblk * fpb;
   const int nb = n / 2 + 1;
   const int woff = (n - J.win) / 2;
@@ -148,7 +267,7 @@ __device__ void stft_bwd_frames_block(const StftJobD& J, int fblk, int b, float2
     a[f * n + k] = g;
   }
   __syncthreads();
-  const float2* out = fft_lds(a, bbuf, tw, n, J.log2n, fpb, +1.f);
+  const float2* out = fft_lds4(a, bbuf, tw, n, J.log2n, fpb, +1.f);
   for (int i = threadIdx.x; i < fpb * n; i += blockDim.x) {
     const int f = i / n;
     const int t = i - f * n;
