@@ -144,16 +144,31 @@ __global__ __launch_bounds__(256) void conv_post_tanh_kernel(const float* __rest
   const int pad = (ksize - 1) / 2;
   const float* xb = x + (int64_t)b * x_bstride;
   for (int i = threadIdx.x; i < channels * ksize; i += 256) wsm[i] = w[i];
-  for (int c = 0; c < channels; ++c) {
-    for (int t = threadIdx.x; t < W; t += 256) {
-      const int tt = t0 - pad + t;
-      float v = 0.f;
-      if (tt >= 0 && tt < t_len) {
-        v = xb[(int64_t)c * x_cstride + tt];
-        v = v < 0.f ? 0.01f * v : v;
+  // 8 channels x 2 window columns per thread in flight at once (a load-use
+  // chain per element serialised ~2 x channels global latencies: 240 us for
+  // the B=16 decoder tail)
+  constexpr int CG = 8;
+  for (int c0 = 0; c0 < channels; c0 += CG) {
+    float v[CG][2];
+#pragma unroll
+    for (int cc = 0; cc < CG; ++cc)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int t = threadIdx.x + 256 * h;
+        const int tt = t0 - pad + t;
+        const bool ok = c0 + cc < channels && t < W && tt >= 0 && tt < t_len;
+        v[cc][h] = ok ? xb[(int64_t)(c0 + cc) * x_cstride + tt] : 0.f;
       }
-      xs[c * W + t] = v;
-    }
+#pragma unroll
+    for (int cc = 0; cc < CG; ++cc)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int t = threadIdx.x + 256 * h;
+        if (c0 + cc < channels && t < W) {
+          const float u = v[cc][h];
+          xs[(c0 + cc) * W + t] = u < 0.f ? 0.01f * u : u;
+        }
+      }
   }
   __syncthreads();
   const int tl = threadIdx.x;
@@ -199,7 +214,7 @@ extern "C" int vits_conv_post_tanh(const float* x, int64_t x_bstride, int32_t x_
                                    const float* w, float* y, int batch, int channels, int t_len,
                                    int ksize, void* stream) {
   VITS_CHECK_ARG(x && w && y && batch > 0 && channels > 0 && t_len > 0 && ksize > 0);
-  VITS_CHECK_SHAPE((ksize & 1) == 1 && x_cstride >= t_len);
+  VITS_CHECK_SHAPE((ksize & 1) == 1 && ksize <= 257 && x_cstride >= t_len);
   const size_t lds = sizeof(float) * ((size_t)channels * (CP_T + ksize - 1) + channels * ksize);
   VITS_CHECK_SHAPE(lds <= 64 * 1024);
   dim3 grid((t_len + CP_T - 1) / CP_T, batch);
