@@ -17,6 +17,8 @@
 namespace {
 
 constexpr int FFT_MAX = 2048;  // complex points per workgroup
+constexpr int STFT_WG = 256;   // threads per workgroup (every launch below)
+constexpr int STFT_PER = FFT_MAX / STFT_WG;  // staged elements per thread
 
 __device__ __forceinline__ int reflect_idx(int i, int L) {
   // torch reflect padding (no edge repeat); valid for |pad| < L
@@ -215,17 +217,25 @@ __device__ void stft_fwd_block(const StftJobD& J, int fblk, int b, float2* sfft)
   const int f0 = fblk * fpb;
   const int woff = (n - J.win) / 2;
   const float* xb = J.x + (int64_t)b * J.L;
-  for (int i = threadIdx.x; i < fpb * n; i += blockDim.x) {
+  // every element's loads issued before the first LDS store (a per-element
+  // load-use chain serialised up to 8 global latencies per workgroup)
+  float xv[STFT_PER], wv[STFT_PER];
+#pragma unroll
+  for (int q = 0; q < STFT_PER; ++q) {
+    const int i = threadIdx.x + q * STFT_WG;
     const int f = i / n;
     const int t = i - f * n;
     const int fr = f0 + f;
-    float v = 0.f;
     const int wi = t - woff;
-    if (fr < J.frames && wi >= 0 && wi < J.win) {
-      const int src = reflect_idx(fr * J.hop + t - J.pad, J.L);
-      v = xb[src] * J.window[wi];
-    }
-    a[i] = make_float2(v, 0.f);
+    const bool ok = i < fpb * n && fr < J.frames && wi >= 0 && wi < J.win;
+    const int src = ok ? reflect_idx(fr * J.hop + t - J.pad, J.L) : 0;
+    xv[q] = ok ? xb[src] : 0.f;
+    wv[q] = ok ? J.window[wi] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < STFT_PER; ++q) {
+    const int i = threadIdx.x + q * STFT_WG;
+    if (i < fpb * n) a[i] = make_float2(xv[q] * wv[q], 0.f);
   }
   __syncthreads();
   const float2* out = fft_lds4(a, bbuf, tw, n, J.log2n, fpb, -1.f);
@@ -254,17 +264,29 @@ __device__ void stft_bwd_frames_block(const StftJobD& J, int fblk, int b, float2
   const int f0 = fblk * fpb;
   const int nb = n / 2 + 1;
   const int woff = (n - J.win) / 2;
-  for (int i = threadIdx.x; i < fpb * n; i += blockDim.x) {
+  float gm[STFT_PER], mg[STFT_PER], rr[STFT_PER], ii[STFT_PER];
+#pragma unroll
+  for (int q = 0; q < STFT_PER; ++q) {
+    const int i = threadIdx.x + q * STFT_WG;
     const int k = i / fpb;  // bin-major so reads along frames are contiguous
     const int f = i - k * fpb;
     const int fr = f0 + f;
-    float2 g = make_float2(0.f, 0.f);
-    if (k < nb && fr < J.frames) {
-      const int64_t o = ((int64_t)b * nb + k) * J.frames + fr;
-      const float sc = J.gmag[o] / J.mag[o];
-      g = make_float2(sc * J.re[o], sc * J.im[o]);
+    const bool ok = i < fpb * n && k < nb && fr < J.frames;
+    const int64_t o = ok ? ((int64_t)b * nb + k) * J.frames + fr : 0;
+    gm[q] = ok ? J.gmag[o] : 0.f;
+    mg[q] = ok ? J.mag[o] : 1.f;
+    rr[q] = ok ? J.re[o] : 0.f;
+    ii[q] = ok ? J.im[o] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < STFT_PER; ++q) {
+    const int i = threadIdx.x + q * STFT_WG;
+    if (i < fpb * n) {
+      const int k = i / fpb;
+      const int f = i - k * fpb;
+      const float sc = gm[q] / mg[q];
+      a[f * n + k] = make_float2(sc * rr[q], sc * ii[q]);
     }
-    a[f * n + k] = g;
   }
   __syncthreads();
   const float2* out = fft_lds4(a, bbuf, tw, n, J.log2n, fpb, +1.f);
