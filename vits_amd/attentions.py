@@ -12,6 +12,7 @@ import torch
 from torch import nn
 from torch.nn import functional as F
 
+from . import train_ops
 from .modules import LayerNorm
 
 
@@ -37,8 +38,10 @@ class MultiHeadAttention(nn.Module):
         nn.init.xavier_uniform_(self.conv_v.weight)
 
     def forward(self, x, c, attn_mask=None):
-        q, k, v = self.conv_q(x), self.conv_k(c), self.conv_v(c)
-        return self.conv_o(self.attention(q, k, v, mask=attn_mask)[0])
+        # 1x1 projections on the HIP training conv under autocast (torch otherwise)
+        conv = train_ops.conv1d
+        q, k, v = conv(self.conv_q, x), conv(self.conv_k, c), conv(self.conv_v, c)
+        return conv(self.conv_o, self.attention(q, k, v, mask=attn_mask)[0])
 
     def attention(self, query, key, value, mask=None):
         b, d, t_s = key.size()
@@ -81,8 +84,9 @@ class FFN2(nn.Module):
         return torch.tanh(xa + sa.unsqueeze(-1)) * torch.sigmoid(xb + sb.unsqueeze(-1))
 
     def forward(self, x, x_mask, g):
-        x = self._gate(self.drop(self.conv_1(x)), g)
-        return self.conv_2(x * x_mask) * x_mask
+        # HIP conv + fused gate under autocast; the reference's ops otherwise
+        x = train_ops.gate(self.drop(train_ops.conv1d(self.conv_1, x)), self.cond(g))
+        return train_ops.conv1d(self.conv_2, x * x_mask) * x_mask
 
     def infer(self, x, g):
         return self.conv_2(self._gate(self.conv_1(x), g))

@@ -64,13 +64,14 @@ class DurationPredictor(nn.Module):
 
     def forward(self, x, x_mask, g):
         x, g = torch.detach(x), torch.detach(g)
-        x = self.pre(x) + self.cond1(g).unsqueeze(-1)
-        x = self.conv_1(x * x_mask)
+        conv = train_ops.conv1d  # HIP under autocast on the GPU, torch otherwise
+        x = conv(self.pre, x) + self.cond1(g).unsqueeze(-1)
+        x = conv(self.conv_1, x * x_mask)
         x = self.drop(self.norm_1(self.act_1(x)))
         x = x + self.cond2(g).unsqueeze(-1)
-        x = self.conv_2(x * x_mask)
+        x = conv(self.conv_2, x * x_mask)
         x = self.drop(self.norm_2(self.act_2(x)))
-        x = self.proj(x * x_mask)
+        x = conv(self.proj, x * x_mask)
         return x * x_mask
 
     @torch.no_grad()
@@ -117,7 +118,7 @@ class TextEncoder(nn.Module):
         x = self.positional_encoding(x, self.alpha).transpose(1, -1)
         x_mask = torch.unsqueeze(commons.sequence_mask(x_lengths, x.size(2)), 1).to(x.dtype)
         x = self.encoder(x * x_mask, x_mask, g=g)
-        stats = self.proj(x) * x_mask
+        stats = train_ops.conv1d(self.proj, x) * x_mask
         m, logs = torch.split(stats, self.out_channels, dim=1)
         return x, m, logs, x_mask
 
