@@ -195,3 +195,47 @@ def test_wgrad_atomic_and_split_modes(device, B, cin, cout, k, dil, pad, T, slop
     F.conv1d(xr, wr, None, padding=pad, dilation=dil).backward(_r16(dy))
     _close(dw, wr.grad, "dw")
     _close(db, dy.sum((0, 2)), "db")
+
+
+@pytest.mark.parametrize("C,O,K,u,T", [(512, 256, 16, 8, 48), (256, 128, 12, 6, 384),
+                                       (128, 64, 4, 2, 2304), (64, 32, 4, 2, 4608),
+                                       (24, 8, 4, 2, 77), (16, 8, 8, 2, 50)])
+def test_conv_transpose1d_train_polyphase(device, C, O, K, u, T):
+    """Generator upsampler in training (train_ops.conv_transpose1d under fp16
+    autocast: polyphase lowering on Conv1dHip, leaky-relu 0.1 prologue fused)
+    against torch's conv_transpose1d in fp32 on the same fp16-rounded
+    operands: output, input, weight and bias gradients."""
+    from torch.nn.utils import weight_norm
+
+    g = torch.Generator().manual_seed(C + O + K + T)
+    m = weight_norm(torch.nn.ConvTranspose1d(C, O, K, u, padding=(K - u) // 2))
+    with torch.no_grad():
+        m.weight_v.copy_(torch.randn(m.weight_v.shape, generator=g))
+        m.weight_g.copy_(torch.rand(m.weight_g.shape, generator=g) + 0.5)
+        m.bias.copy_(torch.randn(O, generator=g) * 0.1)
+    x = torch.randn(2, C, T, generator=g)
+    dy = torch.randn(2, O, T * u, generator=g)
+    md = m.to(device)
+    xd = x.to(device).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = train_ops.conv_transpose1d(md, xd, in_slope=0.1)
+    assert y.dtype == torch.float32 and y.shape == (2, O, T * u)
+    y.backward(dy.to(device))
+
+    w = torch._weight_norm(m.weight_v.detach().cpu(), m.weight_g.detach().cpu(), 0)
+    wr = _r16(w).requires_grad_(True)
+    br = m.bias.detach().cpu().clone().requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    xa = F.leaky_relu(xr, 0.1)
+    xa16 = xa + (_r16(xa.detach()) - xa.detach())
+    yr = F.conv_transpose1d(xa16, wr, br, stride=u, padding=(K - u) // 2)
+    yr.backward(_r16(dy))
+    _close(y, yr, "y")
+    _close(xd.grad, xr.grad, "dx")
+    # d weight_v / weight_g go through the weight-norm reparametrisation on
+    # both sides; compare the effective-weight gradient via the module's
+    w_grad = torch.autograd.grad(
+        torch._weight_norm(md.weight_v, md.weight_g, 0), [md.weight_v, md.weight_g],
+        grad_outputs=wr.grad.to(device), allow_unused=True)
+    _close(md.weight_v.grad, w_grad[0], "dweight_v")
+    _close(md.bias.grad, dy.sum((0, 2)), "db")

@@ -247,7 +247,8 @@ class Generator(nn.Module):
             return engine.generator_forward(self, x, g)
         x = train_ops.conv1d(self.conv_pre, x)
         for i in range(self.num_upsamples):
-            x = self.ups[i](F.leaky_relu(x, modules.LRELU_SLOPE))
+            # polyphase on the HIP training conv under autocast (torch otherwise)
+            x = train_ops.conv_transpose1d(self.ups[i], x, in_slope=modules.LRELU_SLOPE)
             xs = 0
             for j in range(self.num_kernels):
                 xs = xs + self.resblocks[i * self.num_kernels + j](x, g=g)

@@ -270,3 +270,77 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) -> torch.T
     w = weight_norm_effective(module)
     return Conv1dHip.apply(x, w, module.bias, module.dilation[0], module.padding[0], in_slope,
                            wdt)
+
+
+# ---------------------------------------------------------------------------
+# ConvTranspose1d (the Generator's upsamplers, models.py:306-310) in training
+# ---------------------------------------------------------------------------
+
+_POLY_INDEX = {}
+
+
+def _poly_index(K: int, u: int, p: int, device):
+    """Gather map of the polyphase lowering of ConvTranspose1d(K, stride u,
+    padding p): output phase r of channel o is a stride-1 conv of x with
+    P + 1 taps (P = ceil(K / u)), tap i reading x[q - (P - 1 - c0) + i]:
+        W_poly[o*u + r][c][i] = W[c][o][u*m + r'],
+        r' = (r + p) mod u, carry = (r + p) div u, c0 = p div u,
+        m = P - 1 + carry - c0 - i,
+    zero where u*m + r' is not a tap of W (the carries of the phases span
+    c0 .. c0 + 1, hence one extra tap).  Returns (index [u, P+1] into K,
+    valid mask [u, P+1])."""
+    key = (K, u, p, str(device))
+    if key not in _POLY_INDEX:
+        P = (K + u - 1) // u
+        idx = torch.zeros(u, P + 1, dtype=torch.long)
+        ok = torch.zeros(u, P + 1, dtype=torch.bool)
+        c0 = p // u
+        for r in range(u):
+            rp, carry = (r + p) % u, (r + p) // u
+            for i in range(P + 1):
+                m = P - 1 + carry - c0 - i
+                j = u * m + rp
+                if 0 <= m < P and 0 <= j < K:
+                    idx[r, i], ok[r, i] = j, True
+        _POLY_INDEX[key] = (idx.to(device), ok.to(device))
+    return _POLY_INDEX[key]
+
+
+def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) -> torch.Tensor:
+    """``module(leaky_relu(x, in_slope))`` for an nn.ConvTranspose1d
+    (optionally legacy-weight-normed, output_padding 0, groups 1, dilation 1).
+
+    Inside a 16-bit autocast region on a ROCm device: the polyphase lowering
+    on the HIP training conv - one stride-1 Conv1dHip (forward, input and
+    weight gradient on MFMA) over phase-stacked weight rows, the leaky-relu
+    fused as its prologue, then one interleave of the phases into time.
+    The weight gradient flows back through the (differentiable) gather that
+    builds the phase weights.  Elsewhere: the torch module (MIOpen / CPU)."""
+    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+    ok = (isinstance(module, nn.ConvTranspose1d) and module.groups == 1
+          and module.dilation == (1,) and module.output_padding == (0,)
+          and module.padding_mode == "zeros")
+    if wdt is None or not ok:
+        if in_slope != 1.0:
+            x = F.leaky_relu(x, in_slope)
+        return module(x)
+    u, K, p = module.stride[0], module.kernel_size[0], module.padding[0]
+    P = (K + u - 1) // u
+    c0 = p // u
+    # conv padding P - 1 - c0 must leave >= T outputs per phase
+    if (P < 2 + 2 * c0 or not _lib_k_ok(P + 1, 1)
+            or (x.shape[2] - 1) * u - 2 * p + K != x.shape[2] * u):
+        if in_slope != 1.0:
+            x = F.leaky_relu(x, in_slope)
+        return module(x)
+    w = weight_norm_effective(module)                  # [C, O, K]
+    C, O = w.shape[0], w.shape[1]
+    idx, valid = _poly_index(K, u, p, w.device)        # [u, P+1]
+    wt = w.permute(1, 0, 2)                            # [O, C, K]
+    wp = wt[:, :, idx] * valid.to(w.dtype)             # [O, C, u, P+1]
+    wp = wp.permute(0, 2, 1, 3).reshape(O * u, C, P + 1)
+    bias = None if module.bias is None else module.bias.repeat_interleave(u)
+    B, _, T = x.shape
+    y = Conv1dHip.apply(x, wp, bias, 1, P - 1 - c0, in_slope, wdt)  # [B, O*u, >= T]
+    # phases -> time: y[b][o*u + r][q] -> out[b][o][q*u + r]  (T_out = T*u)
+    return y[:, :, :T].reshape(B, O, u, T).permute(0, 1, 3, 2).reshape(B, O, T * u)
