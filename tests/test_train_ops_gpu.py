@@ -8,6 +8,7 @@ dbias, which the kernel sums in fp32 before rounding)."""
 import pytest
 import torch
 import torch.nn.functional as F
+import torch.nn.functional as F_
 
 from vits_amd import train_ops
 
@@ -239,3 +240,35 @@ def test_conv_transpose1d_train_polyphase(device, C, O, K, u, T):
         grad_outputs=wr.grad.to(device), allow_unused=True)
     _close(md.weight_v.grad, w_grad[0], "dweight_v")
     _close(md.bias.grad, dy.sum((0, 2)), "db")
+
+
+@pytest.mark.parametrize("C,F,T,k0,s0", [(1, 65, 289, 5, 2), (1, 1025, 19, 5, 2),
+                                         (64, 31, 145, 5, 2), (1, 257, 73, 7, 3)])
+def test_conv2d_freq_unfolded(device, C, F, T, k0, s0):
+    """STFT-discriminator Conv2d(C, 64, (k0, 5), stride (s0, 1), padding (0, 2))
+    as the unfolded stride-1 Conv1d on the HIP training conv
+    (discriminators.conv2d_freq): output, magnitude gradient, weight and bias
+    gradients vs torch conv2d in fp32 on the same fp16-rounded operands."""
+    import vits_amd.discriminators as D
+
+    g = torch.Generator().manual_seed(C * 1000 + F + k0)
+    layer = torch.nn.Conv2d(C, 64, (k0, 5), stride=(s0, 1), padding=(0, 2))
+    with torch.no_grad():
+        layer.weight.copy_(torch.randn(layer.weight.shape, generator=g) / (C * k0 * 5) ** 0.5)
+        layer.bias.copy_(torch.randn(64, generator=g) * 0.1)
+    x = torch.rand(2, C, F, T, generator=g)
+    F_out = (F - k0) // s0 + 1
+    dy = torch.randn(2, 64, F_out, T, generator=g)
+    ld = layer.to(device)
+    xd = x.to(device).requires_grad_(True)
+    y = D.conv2d_freq(ld, xd, train_ops.TRAIN_WDTYPE)
+    y.backward(dy.to(device))
+    wr = _r16(layer.weight.detach().cpu()).requires_grad_(True)
+    br = layer.bias.detach().cpu().clone().requires_grad_(True)
+    xr = _r16(x).requires_grad_(True)
+    yr = F_.conv2d(xr, wr, br, stride=(s0, 1), padding=(0, 2))
+    yr.backward(_r16(dy))
+    _close(y, yr, "y")
+    _close(xd.grad, xr.grad, "dx")
+    _close(ld.weight.grad, wr.grad, "dw")
+    _close(ld.bias.grad, dy.sum((0, 2, 3)), "db")

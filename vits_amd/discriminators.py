@@ -106,7 +106,48 @@ class STFTDiscriminator(nn.Module):
         _xavier_reset(self)
 
     def forward(self, x):
-        return self.convs(x.unsqueeze(1)).squeeze_(1).squeeze_(2)
+        h = x.unsqueeze(1)
+        layers = list(self.convs)
+        first = layers[0]
+        wdt = train_ops.autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+        if STFT_D_HIP and wdt is not None and _freq_conv_ok(first):
+            # the 1-channel first layer (its data-gradient was CK's slowest
+            # conv kernel in the step) on the HIP training conv
+            h = conv2d_freq(first, h, wdt)
+            layers = layers[1:]
+        for layer in layers:
+            h = layer(h)
+        return h.squeeze(1).squeeze(2)  # [B, 1, T] as mrd.py:156
+
+
+STFT_D_HIP = True  # test switch: False keeps every STFT-discriminator conv on torch
+
+
+def _freq_conv_ok(layer) -> bool:
+    return (isinstance(layer, Conv2d) and layer.groups == 1 and layer.dilation == (1, 1)
+            and layer.stride[1] == 1 and layer.padding[0] == 0
+            and layer.padding_mode == "zeros" and not layer._forward_pre_hooks
+            and train_ops._lib_k_ok(layer.kernel_size[1], 1))
+
+
+def conv2d_freq(layer, h, wdt):
+    """Conv2d(C, O, (k0, k1), stride (s0, 1), padding (0, p1)) over [B, C, F, T]
+    as ONE stride-1 Conv1d along time: the frequency windows are unfolded
+    into channels ([B * F_out, C * k0, T]) and the weight [O, C, k0, k1] is
+    read as [O, C * k0, k1].  Forward, data and weight gradient run on the
+    HIP training conv (Conv1dHip); the unfold's backward folds the data
+    gradient back onto the frequency axis.  Returns [B, O, F_out, T] (a
+    permuted view)."""
+    B, C, F_, T = h.shape
+    O = layer.out_channels
+    k0, k1 = layer.kernel_size
+    s0 = layer.stride[0]
+    F_out = (F_ - k0) // s0 + 1
+    u = h.unfold(2, k0, s0)                                    # [B, C, F_out, T, k0]
+    u = u.permute(0, 2, 1, 4, 3).reshape(B * F_out, C * k0, T)
+    w = layer.weight.reshape(O, C * k0, k1)
+    y = train_ops.Conv1dHip.apply(u, w, layer.bias, 1, layer.padding[1], 1.0, wdt)
+    return y.view(B, F_out, O, y.shape[2]).permute(0, 2, 1, 3)
 
 
 class MultiSTFTDiscriminator(nn.Module):
