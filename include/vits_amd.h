@@ -293,6 +293,12 @@ int vits_attention_forward(const float* q, const float* k, const float* v, float
 int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, void* out,
                        int m_pad, int cin_pad, int wdtype, float* zero, int64_t zero_n,
                        void* stream);
+/* Both images in one launch: `out` as transpose = 0 ([cin_pad/16][k][2]   */
+/* [m_pad][8], rows cout) and `out_t` as transpose = 1 (rows cin, channels  */
+/* cout) -- the training forward packs its backward's image with it.       */
+int vits_conv1d_pack16_pair(const float* w, int cout, int cin, int k, void* out, int m_pad,
+                            int cin_pad, void* out_t, int m_pad_t, int cin_pad_t, int wdtype,
+                            void* stream);
 
 typedef struct vits_conv1d_wgrad_desc {
   const float* dy;        /* output gradient [B][cout][n_out], t contiguous  */

@@ -200,6 +200,11 @@ _SIGS = {
         [C.c_void_p] + [C.c_int] * 4 + [C.c_void_p] + [C.c_int] * 3
         + [C.c_void_p, C.c_int64, C.c_void_p],
     ),
+    "vits_conv1d_pack16_pair": (
+        C.c_int,
+        [C.c_void_p] + [C.c_int] * 3 + [C.c_void_p] + [C.c_int] * 2 + [C.c_void_p]
+        + [C.c_int] * 3 + [C.c_void_p],
+    ),
     "vits_conv1d_wgrad": (C.c_int, [C.POINTER(ConvWgradDesc), C.c_int, C.c_void_p]),
     "vits_conv1d_wgrad_workspace": (C.c_int64, [C.POINTER(ConvWgradDesc), C.c_int]),
     "vits_conv1d_wgrad_split": (C.c_int, [C.POINTER(ConvWgradDesc), C.c_int, C.c_void_p,

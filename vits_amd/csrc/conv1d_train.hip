@@ -362,6 +362,46 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
 }
 
 // ---- weight image for the 16-bit forward kernel ------------------------------
+// element i of the image out[c/16][j][(c%16)/8][m][c%8] (rows m / channels c
+// are (co, ci) or, transposed, (ci, co) with the tap order reversed)
+template <typename T>
+__device__ __forceinline__ void pack16_elem(const float* __restrict__ w, int cout, int cin, int k,
+                                            int transpose, T* __restrict__ out, int m_pad,
+                                            int64_t i) {
+  const int c8 = (int)(i & 7);
+  int64_t r = i >> 3;
+  const int m = (int)(r % m_pad);
+  r /= m_pad;
+  const int half = (int)(r & 1);
+  r >>= 1;
+  const int j = (int)(r % k);
+  const int cg = (int)(r / k);
+  const int c = cg * 16 + half * 8 + c8;
+  float v = 0.f;
+  if (!transpose) {
+    if (m < cout && c < cin) v = w[((int64_t)m * cin + c) * k + j];
+  } else {
+    if (m < cin && c < cout) v = w[((int64_t)c * cin + m) * k + (k - 1 - j)];
+  }
+  out[i] = (T)v;
+}
+
+// both images (forward and transposed / tap-reversed for the input
+// gradient) in ONE launch: the training forward packs the backward's image
+// too, one graph node instead of two per conv
+template <typename T>
+__global__ void pack16_pair_kernel(const float* __restrict__ w, int cout, int cin, int k,
+                                   T* __restrict__ out, int m_pad, int64_t total,
+                                   T* __restrict__ out_t, int m_pad_t, int64_t total_t) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total + total_t;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < total)
+      pack16_elem<T>(w, cout, cin, k, 0, out, m_pad, i);
+    else
+      pack16_elem<T>(w, cout, cin, k, 1, out_t, m_pad_t, i - total);
+  }
+}
+
 template <typename T>
 __global__ void pack16_kernel(const float* __restrict__ w, int cout, int cin, int k, int transpose,
                               T* __restrict__ out, int m_pad, int cin_pad,
@@ -455,6 +495,31 @@ extern "C" int vits_conv1d_wgrad_split(const vits_conv1d_wgrad_desc* d, int batc
     VITS_RED_CASE(64)
 #undef VITS_RED_CASE
   }
+  return vits_launch_status();
+}
+
+extern "C" int vits_conv1d_pack16_pair(const float* w, int cout, int cin, int k, void* out,
+                                       int m_pad, int cin_pad, void* out_t, int m_pad_t,
+                                       int cin_pad_t, int wdtype, void* stream) {
+  VITS_CHECK_ARG(w && out && out_t && cout > 0 && cin > 0 && k > 0);
+  VITS_CHECK_SHAPE(m_pad % 128 == 0 && m_pad >= cout && cin_pad % 16 == 0 && cin_pad >= cin);
+  VITS_CHECK_SHAPE(m_pad_t % 128 == 0 && m_pad_t >= cin && cin_pad_t % 16 == 0 &&
+                   cin_pad_t >= cout);
+  const int64_t total = (int64_t)cin_pad * k * m_pad;
+  const int64_t total_t = (int64_t)cin_pad_t * k * m_pad_t;
+  const int64_t nblk = (total + total_t + 255) / 256;
+  const int blocks = (int)(nblk < 8192 ? nblk : 8192);
+  hipStream_t s = as_stream(stream);
+  if (wdtype == VITS_WDT_F16)
+    hipLaunchKernelGGL(pack16_pair_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, w, cout, cin,
+                       k, reinterpret_cast<_Float16*>(out), m_pad, total,
+                       reinterpret_cast<_Float16*>(out_t), m_pad_t, total_t);
+  else if (wdtype == VITS_WDT_BF16)
+    hipLaunchKernelGGL(pack16_pair_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, w, cout, cin, k,
+                       reinterpret_cast<__bf16*>(out), m_pad, total,
+                       reinterpret_cast<__bf16*>(out_t), m_pad_t, total_t);
+  else
+    return VITS_E_ARG;
   return vits_launch_status();
 }
 

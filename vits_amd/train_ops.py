@@ -61,6 +61,27 @@ def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype:
                       _pick_tile_bf16(rows, k), 16, out_channels=rows, wdtype=wdtype)
 
 
+def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
+                 bias: torch.Tensor | None):
+    """The forward image and the input-gradient (transposed, tap-reversed)
+    image of one weight in ONE launch: (forward PackedConv, backward
+    PackedConv)."""
+    cout, cin, k = w32.shape
+    dt = _TORCH_16[wdtype]
+    m_pad, cin_pad = (cout + 127) // 128 * 128, (cin + 15) // 16 * 16
+    m_pad_t, cin_pad_t = (cin + 127) // 128 * 128, (cout + 15) // 16 * 16
+    img = torch.empty(cin_pad // 16, k, 2, m_pad, 8, dtype=dt, device=w32.device)
+    img_t = torch.empty(cin_pad_t // 16, k, 2, m_pad_t, 8, dtype=dt, device=w32.device)
+    check(_lib.load().vits_conv1d_pack16_pair(
+        w32.data_ptr(), cout, cin, k, img.data_ptr(), m_pad, cin_pad, img_t.data_ptr(), m_pad_t,
+        cin_pad_t, wdtype, _stream_ptr(w32.device)), "vits_conv1d_pack16_pair")
+    fwd = PackedConv(img, bias, cin, cout, k, dil, pad_left, EPI_STORE,
+                     _pick_tile_bf16(cout, k), 16, out_channels=cout, wdtype=wdtype)
+    bwd = PackedConv(img_t, None, cout, cin, k, dil, (k - 1) * dil - pad_left, EPI_STORE,
+                     _pick_tile_bf16(cin, k), 16, out_channels=cin, wdtype=wdtype)
+    return fwd, bwd
+
+
 def _run(x: torch.Tensor, layer: PackedConv, n_out: int, in_slope: float = 1.0,
          gmask: torch.Tensor | None = None, gmask_slope: float = 1.0) -> torch.Tensor:
     B = x.shape[0]
@@ -151,7 +172,13 @@ class Conv1dHip(torch.autograd.Function):
         k = w32.shape[2]
         n_out = x.shape[2] + 2 * padding - (k - 1) * dilation
         b32 = None if bias is None else bias.detach().contiguous()
-        layer = _pack16(w32, False, dilation, padding, wdtype, b32)
+        if ctx.needs_input_grad[0]:
+            # the backward's input-gradient image is packed in the same launch
+            layer, layer_t = _pack16_pair(w32, dilation, padding, wdtype, b32)
+            ctx.layer_t = layer_t
+        else:
+            layer = _pack16(w32, False, dilation, padding, wdtype, b32)
+            ctx.layer_t = None
         y = _run(x, layer, n_out, in_slope)
         ctx.save_for_backward(x, w32)
         ctx.conf = (dilation, padding, in_slope, wdtype, bias is not None)
@@ -172,7 +199,10 @@ class Conv1dHip(torch.autograd.Function):
             # the atomic weight-gradient accumulator is cleared by the packing launch
             if want_w and not split:
                 buf = wgrad_buffer(cout, cin, k, has_bias, dy.device, zeroed=False)
-            layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, zero=buf)
+            layer_t = ctx.layer_t
+            if layer_t is None or buf is not None:
+                layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, zero=buf)
+            ctx.layer_t = None
             dx = _run(dy, layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
                       gmask_slope=slope)
         if want_w:
