@@ -37,7 +37,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from ._lib import EPI_STORE, WDT_BF16, WDT_F16, ConvWgradDesc, check
+from ._lib import EPI_STORE, TILE_64x128, TILE_128x128, WDT_BF16, WDT_F16, ConvWgradDesc, check
 from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, conv1d_launch, make_desc, make_out,
                   weight_norm_effective)
 
@@ -45,8 +45,23 @@ _TORCH_16 = {WDT_F16: torch.float16, WDT_BF16: torch.bfloat16}
 TRAIN_WDTYPE = WDT_F16  # the reference's autocast dtype (train_stft.py:165)
 
 
+def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
+    """16-bit tile for the training convs (tools/train_tile_sweep.py on
+    MI355X): the inference rule (_pick_tile_bf16, tuned on long outputs)
+    except short outputs on >= 128 rows with k <= 5 run as 128x128 (the
+    FFN2 conv at T=100: 193 -> 266 TF/s; a 256-column tile is mostly
+    padding there) and 128-row k <= 7 convs as 64x128 (ResBlock stage 2,
+    k7: 307 -> 377 TF/s)."""
+    if m > 32 and n_out is not None and n_out <= 128:
+        return TILE_128x128 if (m >= 128 and k <= 5) else TILE_64x128
+    if 64 < m <= 128 and 3 < k <= 7:
+        return TILE_64x128
+    return _pick_tile_bf16(m, k)
+
+
 def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype: int,
-            bias: torch.Tensor | None = None, zero: torch.Tensor | None = None) -> PackedConv:
+            bias: torch.Tensor | None = None, zero: torch.Tensor | None = None,
+            n_out: int | None = None) -> PackedConv:
     """16-bit weight image (and, in the same launch, clear ``zero``)."""
     cout, cin, k = w32.shape
     rows, chans = (cin, cout) if transpose else (cout, cin)
@@ -58,11 +73,11 @@ def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype:
         None if zero is None else zero.data_ptr(), 0 if zero is None else zero.numel(),
         _stream_ptr(w32.device)), "vits_conv1d_pack16")
     return PackedConv(img, bias, chans, rows, k, dil, pad_left, EPI_STORE,
-                      _pick_tile_bf16(rows, k), 16, out_channels=rows, wdtype=wdtype)
+                      _pick_tile_train(rows, k, n_out), 16, out_channels=rows, wdtype=wdtype)
 
 
 def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
-                 bias: torch.Tensor | None):
+                 bias: torch.Tensor | None, n_out: int | None = None, n_in: int | None = None):
     """The forward image and the input-gradient (transposed, tap-reversed)
     image of one weight in ONE launch: (forward PackedConv, backward
     PackedConv)."""
@@ -76,9 +91,9 @@ def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
         w32.data_ptr(), cout, cin, k, img.data_ptr(), m_pad, cin_pad, img_t.data_ptr(), m_pad_t,
         cin_pad_t, wdtype, _stream_ptr(w32.device)), "vits_conv1d_pack16_pair")
     fwd = PackedConv(img, bias, cin, cout, k, dil, pad_left, EPI_STORE,
-                     _pick_tile_bf16(cout, k), 16, out_channels=cout, wdtype=wdtype)
+                     _pick_tile_train(cout, k, n_out), 16, out_channels=cout, wdtype=wdtype)
     bwd = PackedConv(img_t, None, cout, cin, k, dil, (k - 1) * dil - pad_left, EPI_STORE,
-                     _pick_tile_bf16(cin, k), 16, out_channels=cin, wdtype=wdtype)
+                     _pick_tile_train(cin, k, n_in), 16, out_channels=cin, wdtype=wdtype)
     return fwd, bwd
 
 
@@ -174,10 +189,10 @@ class Conv1dHip(torch.autograd.Function):
         b32 = None if bias is None else bias.detach().contiguous()
         if ctx.needs_input_grad[0]:
             # the backward's input-gradient image is packed in the same launch
-            layer, layer_t = _pack16_pair(w32, dilation, padding, wdtype, b32)
+            layer, layer_t = _pack16_pair(w32, dilation, padding, wdtype, b32, n_out, x.shape[2])
             ctx.layer_t = layer_t
         else:
-            layer = _pack16(w32, False, dilation, padding, wdtype, b32)
+            layer = _pack16(w32, False, dilation, padding, wdtype, b32, n_out=n_out)
             ctx.layer_t = None
         y = _run(x, layer, n_out, in_slope)
         ctx.save_for_backward(x, w32)
@@ -201,7 +216,8 @@ class Conv1dHip(torch.autograd.Function):
                 buf = wgrad_buffer(cout, cin, k, has_bias, dy.device, zeroed=False)
             layer_t = ctx.layer_t
             if layer_t is None or buf is not None:
-                layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, zero=buf)
+                layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, zero=buf,
+                                  n_out=x.shape[2])
             ctx.layer_t = None
             dx = _run(dy, layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
                       gmask_slope=slope)
