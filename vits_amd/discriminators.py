@@ -253,12 +253,36 @@ class MultiWaveSTFTDiscriminator(nn.Module):
 
 MPD_LRELU_SLOPE = 0.1  # modules.LRELU_SLOPE (models.py:347,374)
 _MPD_HIP = os.environ.get("VITS_MPD_HIP", "1") != "0"  # diagnostics switch
+MPD_GEMM = os.environ.get("VITS_MPD_GEMM", "1") != "0"  # im2col+GEMM for strided/grouped
 
 
 def _hip_wdtype(x):
     if not _MPD_HIP or x.device.type != "cuda":
         return None
     return train_ops.autocast_wdtype(x.device.type)
+
+
+def conv1d_gemm(x: torch.Tensor, w: torch.Tensor, bias, stride: int, padding: int,
+                groups: int = 1) -> torch.Tensor:
+    """Strided / grouped Conv1d as im2col + batched GEMM (torch matmul, i.e.
+    hipBLASLt under autocast) instead of MIOpen: the windows are a strided
+    view (unfold) of the zero-padded input, copied once into GEMM layout.
+    Used for the MPD's strided and grouped layers, whose MIOpen fp16 solvers
+    are implicated in the eager-mode fault documented in DESIGN.md §4b."""
+    N, C, T = x.shape
+    O, Cg, k = w.shape
+    G = groups
+    if padding:
+        x = F.pad(x, (padding, padding))
+    u = x.unfold(2, k, stride)                                  # [N, C, T_out, k]
+    T_out = u.shape[2]
+    u = u.reshape(N, G, Cg, T_out, k).permute(0, 1, 3, 2, 4).reshape(N, G, T_out, Cg * k)
+    wg = w.reshape(G, O // G, Cg * k).transpose(1, 2)           # [G, Cg*k, O/G]
+    y = torch.matmul(u, wg)                                     # [N, G, T_out, O/G]
+    y = y.permute(0, 1, 3, 2).reshape(N, O, T_out)
+    if bias is not None:
+        y = y + bias.to(y.dtype).view(1, O, 1)
+    return y
 
 
 def _wn_weight(m: nn.Module) -> torch.Tensor:
@@ -315,6 +339,8 @@ class DiscriminatorP(nn.Module):
             s, pd = layer.stride[0], layer.padding[0]
             if s == 1 and _hip_wdtype(x) is not None:
                 x = train_ops.Conv1dHip.apply(x, w, layer.bias, 1, pd, 1.0, _hip_wdtype(x))
+            elif MPD_GEMM and x.device.type == "cuda":
+                x = conv1d_gemm(x, w, layer.bias, s, pd)
             else:
                 x = F.conv1d(x, w, layer.bias, stride=s, padding=pd)
             x = F.leaky_relu(x, MPD_LRELU_SLOPE)
@@ -362,6 +388,10 @@ class DiscriminatorS(nn.Module):
 
     def _conv(self, layer, x):
         if not self.use_spectral_norm and _MPD_HIP:
+            if MPD_GEMM and x.device.type == "cuda" and not train_ops.supported(layer):
+                # strided / grouped / wide-kernel layers: im2col + GEMM
+                return conv1d_gemm(x, _wn_weight(layer), layer.bias, layer.stride[0],
+                                   layer.padding[0], layer.groups)
             return train_ops.conv1d(layer, x)  # HIP when supported + autocast, else torch
         return layer(x)
 
