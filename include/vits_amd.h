@@ -354,7 +354,9 @@ int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t dy_cstride, 
 /* found_inf: device flag of GradScaler's unscale (NULL = never skip);    */
 /* when set, nothing is updated (GradScaler's skip rule, no host sync).   */
 /* grad_scale: device scalar the grads are still multiplied by (NULL =    */
-/* already unscaled).                                                     */
+/* already unscaled).  lr_dev: optional device double read at run time   */
+/* instead of lr (an lr scheduler's in-place update then reaches a        */
+/* captured hipGraph, train_stft.py:127-139 ExponentialLR).               */
 #define VITS_RADAM_MAX 96
 typedef struct vits_radam_tensor {
   float* param;
@@ -364,8 +366,8 @@ typedef struct vits_radam_tensor {
   int64_t numel;
 } vits_radam_tensor;
 int vits_radam_step(const vits_radam_tensor* tensors, int n, float* scal, const float* found_inf,
-                    const float* grad_scale, double lr, double beta1, double beta2, double eps,
-                    double weight_decay, void* stream);
+                    const float* grad_scale, double lr, const double* lr_dev, double beta1,
+                    double beta2, double eps, double weight_decay, void* stream);
 
 /* library introspection */
 const char* vits_amd_version(void);

@@ -1,5 +1,6 @@
 """Shared helpers for the test suite (configs, fixtures, model builders)."""
 import json
+import math
 import os
 
 import numpy as np
@@ -71,3 +72,37 @@ def snr_db(a, ref):
     if noise == 0:
         return float("inf")
     return 10 * np.log10(sig / noise)
+
+
+def radam_ref(params, grads_seq, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, t0=0, state=None):
+    """radam.py:35-99 restated in the reference's arithmetic (fp32 tensors,
+    Python-double scalars).  ``lr`` may be a list (one value per step, an
+    lr scheduler's sequence); ``t0``/``state`` continue from a saved step."""
+    ps = [p.float().clone() for p in params]
+    if state is None:
+        m = [torch.zeros_like(p) for p in ps]
+        v = [torch.zeros_like(p) for p in ps]
+    else:
+        m, v = [x.clone() for x in state[0]], [x.clone() for x in state[1]]
+    for i_step, grads in enumerate(grads_seq):
+        t = t0 + i_step + 1
+        lr_t = lr[i_step] if isinstance(lr, (list, tuple)) else lr
+        b2t = b2 ** t
+        nmax = 2 / (1 - b2) - 1
+        n = nmax - 2 * t * b2t / (1 - b2t)
+        if n >= 5:
+            step = math.sqrt((1 - b2t) * (n - 4) / (nmax - 4) * (n - 2) / n * nmax
+                             / (nmax - 2)) / (1 - b1 ** t)
+        else:
+            step = 1.0 / (1 - b1 ** t)
+        for i, g in enumerate(grads):
+            g = g.float()
+            v[i].mul_(b2).addcmul_(g, g, value=1 - b2)
+            m[i].mul_(b1).add_(g, alpha=1 - b1)
+            if wd:
+                ps[i].add_(ps[i], alpha=-wd * lr_t)
+            if n >= 5:
+                ps[i].addcdiv_(m[i], v[i].sqrt().add_(eps), value=-step * lr_t)
+            else:
+                ps[i].add_(m[i], alpha=-step * lr_t)
+    return ps

@@ -269,8 +269,6 @@ def test_train_step_gpu_fp16(device):
 def test_train_step_mel_variant_gpu_eager_and_graph(device):
     """train.py's variant on the HIP path: eager steps, then the whole step
     captured into one hipGraph and replayed (finite losses, D and G move)."""
-    from vits_amd import commons
-
     hps = tiny_mel_hps()
     st = _make(hps, device, variant="mel")
     batch = [t.to(device) for t in _batch(hps, 4, seed=0)]
@@ -280,18 +278,15 @@ def test_train_step_mel_variant_gpu_eager_and_graph(device):
         assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_mel"])
     st = _make(hps, device, variant="mel", capturable=True)
     st.scaler = torch.amp.GradScaler("cuda", init_scale=64.0)
-    try:
-        st.capture(batch, warmup=2)
-        d_p = [p.detach().clone() for p in st.net_d.parameters()]
-        g_p = [p.detach().clone() for p in st.net_g.parameters()]
-        outs = [{k: v.clone() for k, v in st.replay().items()} for _ in range(3)]
-        torch.cuda.synchronize()
-        for out in outs:
-            assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
-        assert any(not torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
-        assert any(not torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
-    finally:
-        commons.DEVICE_SLICE_RNG = False
+    st.capture(batch, warmup=2)
+    d_p = [p.detach().clone() for p in st.net_d.parameters()]
+    g_p = [p.detach().clone() for p in st.net_g.parameters()]
+    outs = [{k: v.clone() for k, v in st.replay().items()} for _ in range(3)]
+    torch.cuda.synchronize()
+    for out in outs:
+        assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
+    assert any(not torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
+    assert any(not torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
 
 
 def test_grouped_spectral_norm_matches_torch_hooks():
@@ -343,37 +338,101 @@ def test_train_step_graph_capture_and_skip_rule(device):
     decays) and GradScaler's skip rule holds without a host sync - with an
     overflowing loss scale every gradient is inf, so neither optimizer may
     touch its parameters or moments and the scale must back off."""
-    from vits_amd import commons
-
     hps = tiny_hps()
     st = _make(hps, device, capturable=True)
     # a small initial scale so the first replays are not skipped for fp16
     # overflow (GradScaler starts at 2**16 and halves per overflowing step)
     st.scaler = torch.amp.GradScaler("cuda", init_scale=64.0)
     batch = [t.to(device) for t in _batch(hps, 4, seed=0)]
-    try:
-        st.capture(batch, warmup=2)
-        g_p = [p.detach().clone() for p in st.net_g.parameters()]
-        d_p = [p.detach().clone() for p in st.net_d.parameters()]
-        an0 = float(st.net_g.__dict__["_align_noise_t"])
-        outs = [{k: v.clone() for k, v in st.replay().items()} for _ in range(3)]
-        torch.cuda.synchronize()
-        for out in outs:
-            assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
-        assert any(not torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
-        assert any(not torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
-        assert float(st.net_g.__dict__["_align_noise_t"]) < an0
-        # force overflow: every step must be skipped
-        st.scaler._scale.fill_(3.0e38)
-        g_p = [p.detach().clone() for p in st.net_g.parameters()]
-        d_p = [p.detach().clone() for p in st.net_d.parameters()]
-        d_m = [st.optim_d.state[p]["exp_avg"].clone() for p in st.net_d.parameters()]
+    st.capture(batch, warmup=2)
+    g_p = [p.detach().clone() for p in st.net_g.parameters()]
+    d_p = [p.detach().clone() for p in st.net_d.parameters()]
+    an0 = float(st.net_g.__dict__["_align_noise_t"])
+    outs = [{k: v.clone() for k, v in st.replay().items()} for _ in range(3)]
+    torch.cuda.synchronize()
+    for out in outs:
+        assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
+    assert any(not torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
+    assert any(not torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
+    assert float(st.net_g.__dict__["_align_noise_t"]) < an0
+    # force overflow: every step must be skipped
+    st.scaler._scale.fill_(3.0e38)
+    g_p = [p.detach().clone() for p in st.net_g.parameters()]
+    d_p = [p.detach().clone() for p in st.net_d.parameters()]
+    d_m = [st.optim_d.state[p]["exp_avg"].clone() for p in st.net_d.parameters()]
+    st.replay()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
+    assert all(torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
+    assert all(torch.equal(a, st.optim_d.state[p]["exp_avg"])
+               for a, p in zip(d_m, st.net_d.parameters()))
+    assert float(st.scaler._scale) < 3.0e38
+
+
+@pytest.mark.gpu
+def test_train_step_captured_lr_schedule(device):
+    """Under capture both learning rates are device tensors read at replay:
+    end_epoch() (the ExponentialLR decay of train_stft.py:138-139) changes
+    what the replays use; replacing an lr object after capture raises
+    instead of silently keeping the captured value."""
+    hps = tiny_hps()
+    st = _make(hps, device, capturable=True)
+    st.scaler = torch.amp.GradScaler("cuda", init_scale=64.0)
+    batch = [t.to(device) for t in _batch(hps, 4, seed=0)]
+    st.capture(batch, warmup=2)
+    lr_g = st.optim_g.param_groups[0]["lr"]
+    lr_d = st.optim_d.param_groups[0]["lr"]
+    assert isinstance(lr_g, torch.Tensor) and isinstance(lr_d, torch.Tensor)
+    st.replay()
+    st.end_epoch()
+    st.end_epoch()
+    assert st.optim_g.param_groups[0]["lr"] is lr_g  # updated in place
+    assert abs(float(lr_g) - 2e-4 * hps.train.lr_decay ** 2) < 1e-10
+    assert abs(float(lr_d) - 1e-4 * hps.train.lr_decay ** 2) < 1e-14
+    st.replay()
+    torch.cuda.synchronize()
+    st.optim_d.param_groups[0]["lr"] = 5e-5
+    with pytest.raises(RuntimeError):
         st.replay()
-        torch.cuda.synchronize()
-        assert all(torch.equal(a, b) for a, b in zip(g_p, st.net_g.parameters()))
-        assert all(torch.equal(a, b) for a, b in zip(d_p, st.net_d.parameters()))
-        assert all(torch.equal(a, st.optim_d.state[p]["exp_avg"])
-                   for a, p in zip(d_m, st.net_d.parameters()))
-        assert float(st.scaler._scale) < 3.0e38
-    finally:
-        commons.DEVICE_SLICE_RNG = False
+
+
+def test_rand_slice_device_rng_is_per_model():
+    """capture() switches only its own model's slice draws to the device
+    generator (it used to flip a module global for the whole
+    process); another model's forward keeps the reference's host draw."""
+    from vits_amd import commons
+
+    x = torch.arange(2 * 3 * 40, dtype=torch.float32).view(2, 3, 40)
+    torch.manual_seed(11)
+    a, ids_a = commons.rand_slice_segments(x, torch.tensor([40, 30]), 8)
+    torch.manual_seed(11)
+    r = torch.rand([2])
+    assert torch.equal(ids_a, (r * torch.tensor([33, 23])).long())
+    assert torch.equal(a[1, 0], x[1, 0, ids_a[1]:ids_a[1] + 8])
+
+
+@pytest.mark.gpu
+def test_train_step_mel_variant_base_config_eager(device):
+    """train.py's variant at configs/base.json shapes, B=32, eager (no graph):
+    the configuration that hit a GPU memory fault in r01 while the MPD's
+    strided / grouped convs ran on MIOpen.  Three eager steps
+    on the current path (those convs as im2col + GEMM, stride-1 layers on
+    the HIP conv): finite losses, both networks move."""
+    from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
+
+    hps = default_hps()
+    torch.manual_seed(1234)
+    net_g, net_d = build_models(hps, device, "mel")
+    st = TrainStep(hps, net_g, net_d, device, variant="mel")
+    # GradScaler's default 2**16 would skip the first steps for fp16 overflow
+    st.scaler = torch.amp.GradScaler("cuda", init_scale=64.0)
+    batch = [t.to(device) for t in synthetic_batch(hps, 32, seed=0)]
+    g0 = [p.detach().clone() for p in list(net_g.parameters())[:50]]
+    d0 = [p.detach().clone() for p in net_d.parameters()]
+    outs = [st.step(batch) for _ in range(3)]
+    torch.cuda.synchronize()
+    for out in outs:
+        assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_mel"])
+        assert torch.isfinite(out["loss_disc"])
+    assert any(not torch.equal(a, b) for a, b in zip(g0, net_g.parameters()))
+    assert any(not torch.equal(a, b) for a, b in zip(d0, net_d.parameters()))

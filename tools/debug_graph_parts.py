@@ -14,7 +14,7 @@ torch.manual_seed(1234)
 g, d = build_models(hps, dev)
 st = TrainStep(hps, g, d, dev, capturable=True)
 batch = [t.to(dev) for t in synthetic_batch(hps, B, seed=0)]
-commons.DEVICE_SLICE_RNG = True
+g.__dict__["_device_slice_rng"] = True
 g.__dict__["_align_noise_t"] = torch.tensor(0.01, device=dev)
 x, x_lengths, spec, spec_lengths, y, y_lengths, emo, speakers = batch
 

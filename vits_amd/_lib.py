@@ -221,8 +221,8 @@ _SIGS = {
     ),
     "vits_radam_step": (
         C.c_int,
-        [C.POINTER(RadamTensor), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
-        + [C.c_double] * 5 + [C.c_void_p],
+        [C.POINTER(RadamTensor), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
+         C.c_void_p] + [C.c_double] * 4 + [C.c_void_p],
     ),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),

@@ -73,26 +73,24 @@ def slice_segments(x: torch.Tensor, ids_str: torch.Tensor, segment_size: int = 4
     return torch.gather(x, 2, idx)
 
 
-def rand_slice_segments(x: torch.Tensor, x_lengths=None, segment_size: int = 4):
+def rand_slice_segments(x: torch.Tensor, x_lengths=None, segment_size: int = 4,
+                        device_rng: bool = False):
     """Random window per row (commons.py:56-63); same RNG draw as the
-    reference (one torch.rand([b]) on the host generator)."""
+    reference (one torch.rand([b]) on the host generator).  ``device_rng``
+    (set per model by vits_amd.train.TrainStep.capture, for the hipGraph-
+    captured step) draws the window starts on the device instead."""
     b, d, t = x.size()
     if x_lengths is None:
         x_lengths = t
     ids_str_max = x_lengths - segment_size + 1
-    if DEVICE_SLICE_RNG:
-        # graph-captured training step (vits_amd.train.TrainStep.capture): the
-        # draw must come from the device generator so every replay re-draws
+    if device_rng:
+        # graph-captured training step: the draw must come from the device
+        # generator so every replay re-draws
         r = torch.rand([b], device=x.device)
     else:
         r = torch.rand([b]).to(device=x.device)
     ids_str = (r * ids_str_max).to(dtype=torch.long)
     return slice_segments(x, ids_str, segment_size), ids_str
-
-
-# set by TrainStep.capture (hipGraph-captured step): rand_slice_segments then
-# draws its window starts on the device instead of the host generator
-DEVICE_SLICE_RNG = False
 
 
 def gen_sin_table(max_len: int, d_model: int, padding_idx=None) -> torch.Tensor:

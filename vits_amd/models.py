@@ -356,7 +356,9 @@ class SynthesizerTrn(nn.Module):
         m_p = torch.matmul(attn, m_p.transpose(1, 2)).transpose(1, 2)
         logs_p = torch.matmul(attn, logs_p.transpose(1, 2)).transpose(1, 2)
 
-        z_slice, ids_slice = commons.rand_slice_segments(z, y_lengths, self.segment_size)
+        z_slice, ids_slice = commons.rand_slice_segments(
+            z, y_lengths, self.segment_size,
+            device_rng=self.__dict__.get("_device_slice_rng", False))
         o = self.dec(z_slice, g=g)
 
         if noise_flow is None:

@@ -36,7 +36,7 @@ from .discriminators import MultiWaveSTFTDiscriminator
 from .losses import discriminator_loss, feature_loss, generator_loss, kl_loss
 from .mel_processing import mel_spectrogram_torch, spec_to_mel_torch
 from .models import MultiPeriodDiscriminator, SynthesizerTrn
-from .optim import FusedRAdam
+from .optim import FusedRAdam, RAdam
 from .stft_loss import MultiResolutionSTFTLoss
 
 
@@ -77,7 +77,12 @@ class TrainStep:
         self.capturable = bool(capturable) and device.type == "cuda"
         self.graph = None
         self.mstft = MultiResolutionSTFTLoss().to(device)
-        self.optim_g = torch.optim.AdamW(net_g.parameters(), hps.train.learning_rate,
+        # under capture the learning rates are device tensors: the kernels read
+        # them at replay time, so the ExponentialLR schedulers below (which
+        # fill_ tensor lrs in place) keep working on a captured step
+        lr_of = (lambda v: torch.tensor(float(v), device=device)) if self.capturable \
+            else (lambda v: v)
+        self.optim_g = torch.optim.AdamW(net_g.parameters(), lr_of(hps.train.learning_rate),
                                          betas=hps.train.betas, weight_decay=hps.train.weight_decay,
                                          eps=hps.train.eps,
                                          fused=fused_adamw and device.type == "cuda",
@@ -85,15 +90,23 @@ class TrainStep:
         # radam.py's RAdam (train_stft.py:97): one fused HIP launch on the GPU
         # (GradScaler-aware, sync-free); torch's RAdam (same update) on CPU
         if variant == "mel":
-            self.optim_d = torch.optim.AdamW(net_d.parameters(), hps.train.learning_rate,
+            self.optim_d = torch.optim.AdamW(net_d.parameters(), lr_of(hps.train.learning_rate),
                                              betas=hps.train.betas, weight_decay=0,
                                              eps=hps.train.eps,
                                              fused=fused_adamw and device.type == "cuda",
                                              capturable=self.capturable)
         elif device.type == "cuda":
-            self.optim_d = FusedRAdam(net_d.parameters(), 1e-4)
+            self.optim_d = FusedRAdam(
+                net_d.parameters(),
+                torch.tensor(1e-4, device=device, dtype=torch.float64) if self.capturable else 1e-4)
         else:
-            self.optim_d = torch.optim.RAdam(net_d.parameters(), 1e-4)
+            self.optim_d = RAdam(net_d.parameters(), 1e-4)
+        # train_stft.py:127-128 / train.py:135-136; stepped once per epoch by
+        # the caller (end_epoch(), train_stft.py:138-139)
+        self.scheduler_g = torch.optim.lr_scheduler.ExponentialLR(
+            self.optim_g, gamma=hps.train.lr_decay, last_epoch=-1)
+        self.scheduler_d = torch.optim.lr_scheduler.ExponentialLR(
+            self.optim_d, gamma=hps.train.lr_decay, last_epoch=-1)
         if ddp:
             ids = [device.index] if device.type == "cuda" else None
             net_g = DDP(net_g, device_ids=ids)
@@ -113,6 +126,12 @@ class TrainStep:
         self.autocast = lambda enabled=fp16: torch.autocast(device.type, dtype=torch.float16,
                                                             enabled=enabled, cache_enabled=cache)
         self.scaler = torch.amp.GradScaler(device.type, enabled=fp16)
+
+    def end_epoch(self):
+        """The per-epoch lr decay of train_stft.py:138-139; reaches a captured
+        step too (the lrs are device tensors there)."""
+        self.scheduler_g.step()
+        self.scheduler_d.step()
 
     def step(self, batch):
         if self.variant == "mel":
@@ -306,8 +325,10 @@ class TrainStep:
         assert self.capturable, "TrainStep(capturable=True) is required"
         assert not isinstance(self.net_g, DDP), \
             "DDP's hooks are not capturable: use TrainStep(allreduce=True) for multi-process capture"
-        commons.DEVICE_SLICE_RNG = True
         g_mod = self.net_g
+        # this model's rand_slice_segments draws on the device from now on
+        # (every replay re-draws); other models keep the host generator
+        g_mod.__dict__["_device_slice_rng"] = True
         g_mod.__dict__["_align_noise_t"] = torch.tensor(float(g_mod.align_noise),
                                                         device=self.device)
         self.static = [t.to(self.device).clone() for t in batch]
@@ -327,7 +348,21 @@ class TrainStep:
         # (pre-capture) events while this thread captures
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.static_out = self.step(self.static)
+        self._captured_lrs = self._lr_objects()
         return self.static_out
+
+    def _lr_objects(self):
+        return [g["lr"] for o in (self.optim_g, self.optim_d) for g in o.param_groups]
+
+    def _check_lrs(self):
+        """A captured step reads each group's lr tensor at replay time; a
+        group whose lr was replaced by another object (e.g. a float assigned
+        by hand) would silently keep the captured value - refuse that."""
+        for old, new in zip(self._captured_lrs, self._lr_objects()):
+            if new is not old:
+                raise RuntimeError(
+                    "TrainStep.replay: an optimizer's lr was replaced after capture(); update "
+                    "the captured lr tensor in place (lr schedulers do) or capture again")
 
     def _release_autograd_refs(self):
         """Weight-norm / spectral-norm modules keep the last forward's
@@ -348,6 +383,7 @@ class TrainStep:
         if batch is not None:
             for dst, src in zip(self.static, batch):
                 dst.copy_(src, non_blocking=True)
+        self._check_lrs()
         self.graph.replay()
         g_mod = self.net_g
         g_mod.align_noise = max(g_mod.align_noise - g_mod.align_noise_decay, g_mod.align_noise_min)

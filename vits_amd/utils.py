@@ -4,8 +4,11 @@ Mirrors the parts of the reference ``utils.py`` that sit on the inference /
 training drivers' call path (``HParams`` ``utils.py:249-278``,
 ``get_hparams_from_file`` ``utils.py:205-211``, ``load_checkpoint``
 ``utils.py:19-45``, ``save_checkpoint`` ``utils.py:47-57``,
-``latest_checkpoint_path`` ``utils.py:71-78``).  TensorBoard / matplotlib /
-soundfile helpers are out of scope.
+``latest_checkpoint_path`` ``utils.py:71-78``, ``get_hparams``
+``utils.py:152-191``, ``get_logger`` ``utils.py:234-246``, ``summarize``
+``utils.py:60-68``, ``plot_*`` ``utils.py:81-133``), same signatures and
+return values, so ``from vits_amd import utils`` serves the reference's
+``train*.py`` unpacking patterns.
 
 ``deterministic_fill_`` is the key-hashed weight generator used everywhere a
 model needs reproducible weights without shipping a checkpoint: the golden
@@ -14,13 +17,18 @@ apply it to ours, so both sides hold bit-identical parameters.
 """
 from __future__ import annotations
 
+import argparse
 import glob
 import json
+import logging
 import os
+import subprocess
 import zlib
 
 import numpy as np
 import torch
+
+logger = logging.getLogger("vits_amd")
 
 
 # --------------------------------------------------------------------------
@@ -88,29 +96,40 @@ def _unwrap(model):
     return model.module if hasattr(model, "module") else model
 
 
-def load_checkpoint(checkpoint_path, model, optimizer=None, adapt=False):
-    """Load ``{'model', 'iteration', 'optimizer'}``; missing keys keep the
-    current init (``utils.py:33-39``).  ``adapt`` loads weights only."""
+def load_checkpoint(checkpoint_path, model, optimizer=None, *, adapt=False):
+    """Same contract as the reference (``utils.py:19-45``): returns
+    ``(model, optimizer, iteration)``; ``adapt`` loads weights only and
+    reports iteration 1; a key missing from the checkpoint keeps the current
+    init (``utils.py:33-39``); the load is strict otherwise (a shape mismatch
+    raises, as ``load_state_dict(strict=True)`` does in the reference).
+    Unlike the reference the file is read with ``weights_only=True``."""
     assert os.path.isfile(checkpoint_path), checkpoint_path
     ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
-    iteration = ckpt.get("iteration", 1)
-    if optimizer is not None and not adapt and ckpt.get("optimizer") is not None:
+    if "iteration" in ckpt and not adapt:
+        iteration = ckpt["iteration"]
+    else:
+        iteration = 1
+    if "optimizer" in ckpt and ckpt["optimizer"] is not None and optimizer is not None \
+            and not adapt:
         optimizer.load_state_dict(ckpt["optimizer"])
     saved = ckpt["model"]
     target = _unwrap(model)
-    state = target.state_dict()
     new_state = {}
-    for k, v in state.items():
-        if k in saved and saved[k].shape == v.shape:
+    for k, v in target.state_dict().items():
+        if k in saved:
             new_state[k] = saved[k]
         else:
+            logger.info("%s is not in the checkpoint", k)
             new_state[k] = v
-    target.load_state_dict(new_state)
-    lr = optimizer.param_groups[0]["lr"] if optimizer is not None else None
-    return model, optimizer, lr, iteration
+    target.load_state_dict(new_state, strict=True)
+    logger.info("Loaded checkpoint '%s' (iteration %s)", checkpoint_path, iteration)
+    return model, optimizer, iteration
 
 
 def save_checkpoint(model, optimizer, iteration, checkpoint_path):
+    """``utils.py:47-57``: ``{'model', 'iteration', 'optimizer'}``."""
+    logger.info("Saving model and optimizer state at iteration %s to %s",
+                iteration, checkpoint_path)
     torch.save(
         {
             "model": _unwrap(model).state_dict(),
@@ -119,6 +138,175 @@ def save_checkpoint(model, optimizer, iteration, checkpoint_path):
         },
         checkpoint_path,
     )
+
+
+# --------------------------------------------------------------------------
+# CLI / logging / file helpers the training drivers call
+# --------------------------------------------------------------------------
+def get_hparams(init=True, argv=None) -> HParams:
+    """``utils.py:152-191``: ``-c -m -a -d --ckptG --ckptD``; copies the
+    config to ``./logs/<model>/config.json`` (``init``) or reads it back."""
+    parser = argparse.ArgumentParser()
+    parser.add_argument("-c", "--config", type=str, default="./configs/base.json",
+                        help="JSON file for configuration")
+    parser.add_argument("-m", "--model", type=str, required=True, help="Model name")
+    parser.add_argument("-a", "--adapt", action="store_true",
+                        help="Adaptative training or not, default=False.")
+    parser.add_argument("-d", "--use-dur-dis", action="store_true",
+                        help="Use duration discriminator or not, default=False.")
+    parser.add_argument("--ckptG", type=str, required=False,
+                        help="original VITS G checkpoint path")
+    parser.add_argument("--ckptD", type=str, required=False,
+                        help="original VITS D checkpoint path")
+    args = parser.parse_args(argv)
+    model_dir = os.path.join("./logs", args.model)
+    os.makedirs(model_dir, exist_ok=True)
+    config_save_path = os.path.join(model_dir, "config.json")
+    if init:
+        with open(args.config, "r") as f:
+            data = f.read()
+        with open(config_save_path, "w") as f:
+            f.write(data)
+    else:
+        with open(config_save_path, "r") as f:
+            data = f.read()
+    hparams = HParams(**json.loads(data))
+    hparams.model_dir = model_dir
+    hparams.adapt = args.adapt
+    hparams.use_dur_dis = args.use_dur_dis
+    hparams.ckptG = args.ckptG
+    hparams.ckptD = args.ckptD
+    return hparams
+
+
+def get_hparams_from_dir(model_dir) -> HParams:
+    """``utils.py:194-202``."""
+    with open(os.path.join(model_dir, "config.json"), "r") as f:
+        hparams = HParams(**json.load(f))
+    hparams.model_dir = model_dir
+    return hparams
+
+
+def get_logger(model_dir, filename="train.log"):
+    """``utils.py:234-246``: file logger ``<model_dir>/<filename>``; also
+    becomes this module's logger, as in the reference."""
+    global logger
+    logger = logging.getLogger(os.path.basename(model_dir))
+    logger.setLevel(logging.DEBUG)
+    formatter = logging.Formatter("%(asctime)s\t%(name)s\t%(levelname)s\t%(message)s")
+    os.makedirs(model_dir, exist_ok=True)
+    h = logging.FileHandler(os.path.join(model_dir, filename))
+    h.setLevel(logging.DEBUG)
+    h.setFormatter(formatter)
+    logger.addHandler(h)
+    return logger
+
+
+def check_git_hash(model_dir):
+    """``utils.py:214-231``: record / compare the source tree's git hash."""
+    source_dir = os.path.dirname(os.path.dirname(os.path.realpath(__file__)))
+    if not os.path.exists(os.path.join(source_dir, ".git")):
+        logger.warning("%s is not a git repository, therefore hash value comparison "
+                       "will be ignored.", source_dir)
+        return
+    cur_hash = subprocess.getoutput(f"git -C {source_dir} rev-parse HEAD")
+    path = os.path.join(model_dir, "githash")
+    if os.path.exists(path):
+        with open(path) as f:
+            saved_hash = f.read()
+        if saved_hash != cur_hash:
+            logger.warning("git hash values are different. %s(saved) != %s(current)",
+                           saved_hash[:8], cur_hash[:8])
+    else:
+        with open(path, "w") as f:
+            f.write(cur_hash)
+
+
+def summarize(writer, global_step, scalars={}, histograms={}, images={}, audios={},
+              audio_sampling_rate=22050):
+    """``utils.py:60-68`` over any TensorBoard-``SummaryWriter``-like object."""
+    for k, v in scalars.items():
+        writer.add_scalar(k, v, global_step)
+    for k, v in histograms.items():
+        writer.add_histogram(k, v, global_step)
+    for k, v in images.items():
+        writer.add_image(k, v, global_step, dataformats="HWC")
+    for k, v in audios.items():
+        writer.add_audio(k, v, global_step, audio_sampling_rate)
+
+
+def _figure_to_numpy(fig):
+    # the reference's ``np.fromstring(fig.canvas.tostring_rgb())`` is gone from
+    # current matplotlib/numpy; buffer_rgba gives the same HxWx3 image
+    fig.canvas.draw()
+    data = np.asarray(fig.canvas.buffer_rgba())[..., :3].copy()
+    return data
+
+
+def plot_spectrogram_to_numpy(spectrogram):
+    """``utils.py:81-104``."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    fig, ax = plt.subplots(figsize=(10, 2))
+    im = ax.imshow(spectrogram, aspect="auto", origin="lower", interpolation="none")
+    plt.colorbar(im, ax=ax)
+    plt.xlabel("Frames")
+    plt.ylabel("Channels")
+    plt.tight_layout()
+    data = _figure_to_numpy(fig)
+    plt.close(fig)
+    return data
+
+
+def plot_alignment_to_numpy(alignment, info=None):
+    """``utils.py:107-133``."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    fig, ax = plt.subplots(figsize=(6, 4))
+    im = ax.imshow(alignment.transpose(), aspect="auto", origin="lower",
+                   interpolation="none")
+    fig.colorbar(im, ax=ax)
+    xlabel = "Decoder timestep"
+    if info is not None:
+        xlabel += "\n\n" + info
+    plt.xlabel(xlabel)
+    plt.ylabel("Encoder timestep")
+    plt.tight_layout()
+    data = _figure_to_numpy(fig)
+    plt.close(fig)
+    return data
+
+
+def load_wav_to_torch(full_path):
+    """``utils.py:136-139``: float32 samples peak-normalised to 1.  soundfile is
+    absent from this image, so PCM / float WAV is read with scipy."""
+    from scipy.io import wavfile
+
+    sr, x = wavfile.read(full_path)
+    if x.dtype.kind == "i":
+        x = x.astype(np.float32) / float(np.iinfo(x.dtype).max + 1)
+    elif x.dtype.kind == "u":
+        x = (x.astype(np.float32) - 128.0) / 128.0
+    x = x.astype(np.float32)
+    x /= np.abs(x).max()
+    return torch.from_numpy(x), sr
+
+
+def load_filepaths_and_sid(filename, split="|"):
+    """``utils.py:142-145``."""
+    with open(filename, encoding="utf-8") as f:
+        return [line.strip().split(split) for line in f]
+
+
+def load_binfn(filename, dim):
+    """``utils.py:148-149``: raw float32 text vectors ``[N, dim]``."""
+    return np.fromfile(filename, dtype=np.float32).reshape(-1, dim)
 
 
 # --------------------------------------------------------------------------
