@@ -143,6 +143,15 @@ int vits_conv1d_forward(const vits_conv1d_desc* d, int batch, void* stream);
 /* Run `n` conv descriptors back to back on one stream (one host call). */
 int vits_conv1d_forward_seq(const vits_conv1d_desc* d, int n, int batch, void* stream);
 
+/* Run `ngroups` groups of consecutive descriptors (sizes[i] each, <= 3):  */
+/* the members of a group are independent convs (no member reads another's */
+/* output; the three ResBlock2 branches of one Generator stage,            */
+/* models.py:311-313 / modules.py:250-260) and share ONE launch when they  */
+/* have the same tile, epilogue and staging kind, else run in order.       */
+/* Groups run in order.                                                    */
+int vits_conv1d_forward_groups(const vits_conv1d_desc* d, const int32_t* sizes, int ngroups,
+                               int batch, void* stream);
+
 /* ---------------------------------------------------------------------- */
 /* per-utterance conditioning GEMV: y[b][n] = W[n][:] . g[b][:] + bias[n] */
 /* ---------------------------------------------------------------------- */
@@ -347,6 +356,51 @@ int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t dy_cstride, 
                        int64_t x_bstride, int32_t x_cstride, const float* g, int64_t g_bstride,
                        float* dx, int64_t dx_bstride, int32_t dx_cstride, float* dg, int batch,
                        int half_channels, int t_len, void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* One ResBlock2 dilation pair of the Generator as ONE kernel              */
+/* (modules.py:250-260, fp32):                                             */
+/*   y = x + c2(tanh(a + sa) * sigmoid(b + sb)),  (a|b) = c1(lrelu(x,.1)) */
+/* c1 = Conv1d(C, C, k, dil) packed as vits_conv1d_forward's GATE layout  */
+/* ([cin_pad1][k][m_pad1], rows (a_p, b_p) interleaved), c2 = Conv1d(C/2, */
+/* C, k, dil 1, pad (k-1)/2) packed [cin_pad2][k][m_pad2]; b1 / cond are  */
+/* in logical order ([a | b], cond already offset to this pair), b2 [C].  */
+/* accumulate: y += result (then / post_div) - the branch mean of a stage.*/
+/* x: [B][C][T] fp32, T % 4 == 0, 16-byte aligned; y must not alias x.    */
+/* C in {32, 64} (the 64- and 32-channel Generator stages).  Up to 3      */
+/* independent pairs (same C) run as one launch.  kc1 / kc2 from          */
+/* vits_resblock_pair_kc.                                                 */
+/* ---------------------------------------------------------------------- */
+typedef struct vits_resblock_pair_desc {
+  const float* x;
+  int64_t x_bstride;
+  int32_t x_cstride;
+  int32_t t_len;
+  int32_t channels;
+  float in_slope;
+  const float* w1;
+  int32_t m_pad1;
+  int32_t cin_pad1;
+  int32_t kc1;
+  int32_t k;
+  int32_t dil;
+  int32_t kc2;
+  const float* b1;
+  const float* cond;
+  int64_t cond_bstride;
+  const float* w2;
+  int32_t m_pad2;
+  int32_t cin_pad2;
+  const float* b2;
+  float* y;
+  int64_t y_bstride;
+  int32_t y_cstride;
+  int32_t accumulate;
+  float post_div;
+  int32_t reserved;
+} vits_resblock_pair_desc;
+int vits_resblock_pair_forward(const vits_resblock_pair_desc* d, int n, int batch, void* stream);
+int vits_resblock_pair_kc(int channels, int k, int dil, int* kc1, int* kc2);
 
 /* Fused RAdam step (radam.py:35-99, the D optimizer of train_stft.py:97) */
 /* over a list of fp32 tensors, one launch per VITS_RADAM_MAX tensors.     */

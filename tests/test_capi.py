@@ -40,15 +40,17 @@ def test_struct_layout_matches_header():
     import subprocess
     import tempfile
 
-    from vits_amd._lib import ConvDesc, ConvOut, StftJob
+    from vits_amd._lib import ConvDesc, ConvOut, ResblockPairDesc, StftJob
 
     probe = r'''
 #include <stdio.h>
 #include <stddef.h>
 #include "vits_amd.h"
-int main(){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc), sizeof(vits_conv_out),
- offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths),
- offsetof(vits_conv1d_desc, wdtype), sizeof(vits_stft_job), offsetof(vits_stft_job, eps));
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc),
+ sizeof(vits_conv_out), offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths),
+ offsetof(vits_conv1d_desc, wdtype), sizeof(vits_stft_job), offsetof(vits_stft_job, eps),
+ sizeof(vits_resblock_pair_desc), offsetof(vits_resblock_pair_desc, w2),
+ offsetof(vits_resblock_pair_desc, post_div));
  return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -65,3 +67,6 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc), siz
     assert int(out[4]) == ConvDesc.wdtype.offset
     assert int(out[5]) == ctypes.sizeof(StftJob)
     assert int(out[6]) == StftJob.eps.offset
+    assert int(out[7]) == ctypes.sizeof(ResblockPairDesc)
+    assert int(out[8]) == ResblockPairDesc.w2.offset
+    assert int(out[9]) == ResblockPairDesc.post_div.offset

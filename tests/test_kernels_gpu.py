@@ -377,3 +377,75 @@ def test_stft_mag_multi_target_not_differentiable(device):
     spec = (torch.hann_window(256).to(device), 256, 64, 256, None, 1e-7)
     mx, my = ops.stft_mag_multi([x, y], [spec, spec])
     assert mx.requires_grad and not my.requires_grad and my.grad_fn is None
+
+
+def _resblock_pair_ref(x, w1, b1, cond, w2, b2, k, dil):
+    """modules.py:251-259 for one (c1, c2, cs) pair, fp64 on CPU."""
+    x, w1, b1, w2, b2 = (t.double().cpu() for t in (x, w1, b1, w2, b2))
+    xt = F.conv1d(F.leaky_relu(x, 0.1), w1, b1, dilation=dil, padding=(k - 1) * dil // 2)
+    xa, xb = torch.chunk(xt, 2, dim=1)
+    sa, sb = torch.chunk(cond.double().cpu(), 2, dim=1)
+    xt = torch.tanh(xa + sa.unsqueeze(-1)) * torch.sigmoid(xb + sb.unsqueeze(-1))
+    return F.conv1d(xt, w2, b2, padding=(k - 1) // 2) + x
+
+
+@pytest.mark.parametrize("C,k,dil,T", [
+    (32, 3, 1, 12), (32, 11, 5, 300), (64, 7, 3, 2052), (64, 3, 5, 48), (32, 7, 1, 9216),
+    (64, 11, 1, 500),
+])
+def test_resblock_pair_fused(device, C, k, dil, T):
+    """csrc/resblock.hip (c1 -> gate -> c2 -> residual in one kernel, the
+    32/64-channel Generator stages) against the pair in fp64 on CPU: tiles
+    shorter than the sequence, sequence ends inside a tile (c2's zero
+    padding of the gated signal), the three-branch grouped launch and the
+    branch-mean epilogue (accumulate, post_div).  Tolerance 1e-4 of the
+    output magnitude (fp32 MFMA; fast exp-based tanh / sigmoid ~1e-7)."""
+    g = torch.Generator().manual_seed(C + k + dil + T)
+    B = 2
+    packs, refs, xs = [], [], []
+    for j in range(3):
+        x = torch.randn(B, C, T, generator=g) * 0.5
+        w1 = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
+        b1 = torch.randn(C, generator=g) * 0.1
+        w2 = torch.randn(C, C // 2, k, generator=g) / (C * k / 2) ** 0.5
+        b2 = torch.randn(C, generator=g) * 0.1
+        cond = torch.randn(B, C, generator=g) * 0.3
+        c1 = ops.pack_conv(w1.to(device), b1.to(device), dilation=dil, gate=True)
+        c2 = ops.pack_conv(w2.to(device), b2.to(device))
+        assert k > ops.RESBLOCK_PAIR_MAX_K or ops.resblock_pair_supported(c1, c2, T)
+        packs.append((c1, c2, cond.to(device)))
+        refs.append(_resblock_pair_ref(x, w1, b1, cond, w2, b2, k, dil))
+        xs.append(x.to(device))
+    ys = [torch.full((B, C, T), float("nan"), device=device) for _ in range(3)]
+    ops.resblock_pair_launch(tuple(
+        ops.resblock_pair_desc(c1, c2, xs[j], ys[j], cond=cd) for j, (c1, c2, cd) in enumerate(packs)),
+        B, device)
+    torch.cuda.synchronize()
+    for j in range(3):
+        _close(ys[j], refs[j], what=f"pair {j}")
+    # branch mean into one buffer: y = (r0 + r1 + r2) / 3
+    acc = torch.empty(B, C, T, device=device)
+    for j, (c1, c2, cd) in enumerate(packs):
+        ops.resblock_pair_launch(ops.resblock_pair_desc(
+            c1, c2, xs[j], acc, cond=cd, accumulate=j > 0, post_div=3.0 if j == 2 else 1.0),
+            B, device)
+    torch.cuda.synchronize()
+    _close(acc, (refs[0] + refs[1] + refs[2]) / 3, what="mean")
+
+
+def test_generator_fused_pairs_match_two_conv_path(device, monkeypatch):
+    """The Generator with fused pairs on its 32/64-channel stages equals the
+    two-conv path (VITS_FUSED_PAIRS=0) to fp32 rounding."""
+    from common import base_model
+    from vits_amd import engine
+
+    m = base_model(device)
+    g = torch.Generator().manual_seed(3)
+    z = (torch.randn(2, 192, 40, generator=g) * 0.7).to(device)
+    gg = (torch.randn(2, 1024, generator=g) * 0.5).to(device)
+    with torch.no_grad():
+        monkeypatch.setattr(engine, "_FUSED_PAIRS", True)
+        a = m.dec(z, gg)
+        monkeypatch.setattr(engine, "_FUSED_PAIRS", False)
+        b = m.dec(z, gg)
+    _close(a, b, what="fused vs two-conv")

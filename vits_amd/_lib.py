@@ -11,6 +11,8 @@ import os
 import threading
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libvits_amd.so")
+# A/B experiments (tools/ab_conv.sh) point this at an alternative build
+_LIB_PATH = os.environ.get("VITS_AMD_LIB", _LIB_PATH)
 _lock = threading.Lock()
 _lib = None
 
@@ -80,6 +82,38 @@ class ConvDesc(C.Structure):
     ]
 
 
+class ResblockPairDesc(C.Structure):
+    """include/vits_amd.h vits_resblock_pair_desc."""
+    _fields_ = [
+        ("x", C.c_void_p),
+        ("x_bstride", C.c_int64),
+        ("x_cstride", C.c_int32),
+        ("t_len", C.c_int32),
+        ("channels", C.c_int32),
+        ("in_slope", C.c_float),
+        ("w1", C.c_void_p),
+        ("m_pad1", C.c_int32),
+        ("cin_pad1", C.c_int32),
+        ("kc1", C.c_int32),
+        ("k", C.c_int32),
+        ("dil", C.c_int32),
+        ("kc2", C.c_int32),
+        ("b1", C.c_void_p),
+        ("cond", C.c_void_p),
+        ("cond_bstride", C.c_int64),
+        ("w2", C.c_void_p),
+        ("m_pad2", C.c_int32),
+        ("cin_pad2", C.c_int32),
+        ("b2", C.c_void_p),
+        ("y", C.c_void_p),
+        ("y_bstride", C.c_int64),
+        ("y_cstride", C.c_int32),
+        ("accumulate", C.c_int32),
+        ("post_div", C.c_float),
+        ("reserved", C.c_int32),
+    ]
+
+
 class StftJob(C.Structure):
     _fields_ = [
         ("x", C.c_void_p),
@@ -139,6 +173,8 @@ class RadamTensor(C.Structure):
 _SIGS = {
     "vits_conv1d_forward": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_void_p]),
     "vits_conv1d_forward_seq": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_int, C.c_void_p]),
+    "vits_conv1d_forward_groups": (
+        C.c_int, [C.POINTER(ConvDesc), C.POINTER(C.c_int32), C.c_int, C.c_int, C.c_void_p]),
     "vits_linear_forward": (
         C.c_int,
         [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int,
@@ -219,6 +255,10 @@ _SIGS = {
         [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64,
          C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p],
     ),
+    "vits_resblock_pair_forward": (
+        C.c_int, [C.POINTER(ResblockPairDesc), C.c_int, C.c_int, C.c_void_p]),
+    "vits_resblock_pair_kc": (
+        C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vits_radam_step": (
         C.c_int,
         [C.POINTER(RadamTensor), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,

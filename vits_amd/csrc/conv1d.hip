@@ -18,6 +18,10 @@
 // LDS once; every tap j then reads the same X rows shifted by j*dil, so the
 // input is fetched once per chunk regardless of the kernel width.
 //
+// vits_conv1d_forward_groups runs independent convs of one kind (the three
+// ResBlock2 branches of a Generator stage) as one grid: blockIdx.z selects
+// the member descriptor and the utterance.
+//
 // Reference call sites: modules.py:136,148 (WN in/res_skip convs),
 // modules.py:252,257 (ResBlock2 convs1/convs2), models.py:307,310
 // (conv_pre, ups), modules.py:363,366 (coupling pre/post).
@@ -43,31 +47,64 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   return VITS_OK;
 }
 
-int conv1d_one(const vits_conv1d_desc& d, int batch, hipStream_t s) {
-  int rc = check_desc(d, batch);
-  if (rc) return rc;
-  switch (d.wdtype) {
-    case VITS_WDT_BF16:
-      return vits_conv1d_dispatch_bf16(d, batch, s);
-    case VITS_WDT_F16:
-      return vits_conv1d_dispatch_f16(d, batch, s);
-    default:
-      return vits_conv1d_dispatch_f32(d, batch, s);
+int conv1d_group(const vits_conv1d_desc* d, int n, int batch, hipStream_t s) {
+  vits_conv::ConvGroup g;
+  g.n = n;
+  g.batch = batch;
+  for (int i = 0; i < n; ++i) {
+    int rc = check_desc(d[i], batch);
+    if (rc) return rc;
+    g.d[i] = d[i];
   }
+  switch (d[0].wdtype) {
+    case VITS_WDT_BF16:
+      return vits_conv1d_dispatch_bf16(g, s);
+    case VITS_WDT_F16:
+      return vits_conv1d_dispatch_f16(g, s);
+    default:
+      return vits_conv1d_dispatch_f32(g, s);
+  }
+}
+
+// a group that cannot share one grid (different tiles / epilogues / staging
+// kinds) runs as separate launches, in order
+int conv1d_group_or_seq(const vits_conv1d_desc* d, int n, int batch, hipStream_t s) {
+  if (n > 1 && n <= vits_conv::VITS_CONV_GROUP) {
+    int rc = conv1d_group(d, n, batch, s);
+    if (rc != VITS_E_UNSUP) return rc;
+  }
+  for (int i = 0; i < n; ++i) {
+    int rc = conv1d_group(d + i, 1, batch, s);
+    if (rc) return rc;
+  }
+  return VITS_OK;
 }
 
 }  // namespace
 
 extern "C" int vits_conv1d_forward(const vits_conv1d_desc* d, int batch, void* stream) {
   if (!d) return VITS_E_ARG;
-  return conv1d_one(*d, batch, as_stream(stream));
+  return conv1d_group(d, 1, batch, as_stream(stream));
 }
 
 extern "C" int vits_conv1d_forward_seq(const vits_conv1d_desc* d, int n, int batch, void* stream) {
   if (!d || n < 0) return VITS_E_ARG;
   for (int i = 0; i < n; ++i) {
-    int rc = conv1d_one(d[i], batch, as_stream(stream));
+    int rc = conv1d_group(d + i, 1, batch, as_stream(stream));
     if (rc) return rc;
+  }
+  return VITS_OK;
+}
+
+extern "C" int vits_conv1d_forward_groups(const vits_conv1d_desc* d, const int32_t* sizes,
+                                          int ngroups, int batch, void* stream) {
+  if (!d || !sizes || ngroups < 0) return VITS_E_ARG;
+  int off = 0;
+  for (int i = 0; i < ngroups; ++i) {
+    VITS_CHECK_ARG(sizes[i] >= 1);
+    int rc = conv1d_group_or_seq(d + off, sizes[i], batch, as_stream(stream));
+    if (rc) return rc;
+    off += sizes[i];
   }
   return VITS_OK;
 }

@@ -78,8 +78,24 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
 }
 
+// Up to VITS_CONV_GROUP descriptors of one tile / epilogue / staging kind run
+// as ONE launch (blockIdx.z = group member * batch + utterance): the three
+// ResBlock2 branches of a Generator stage (k = 3, 7, 11) are independent
+// until their mean, so their convs of one pair index share a grid - three
+// times the workgroups of a single conv (the 256-channel stage alone is
+// 1024 workgroups: 1.3 rounds of the chip's resident slots).
+constexpr int VITS_CONV_GROUP = 3;
+struct ConvGroup {
+  vits_conv1d_desc d[VITS_CONV_GROUP];
+  int n;      // members
+  int batch;  // utterances per member
+};
+
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4>
-__global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_desc p) {
+__global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) {
+  const int gi = (int)blockIdx.z / G.batch;
+  const vits_conv1d_desc& p = G.d[gi];
+  if ((int)blockIdx.x * BN >= p.n_out || (int)blockIdx.y * BM >= p.m) return;
   constexpr bool BF = WT != VITS_WDT_F32;  // 16-bit operands (bf16 or fp16)
   typedef typename LowP<WT>::T lp_t;
   typedef lp_t lpx8 __attribute__((ext_vector_type(8)));
@@ -115,7 +131,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
   float* const stage0 = smem;
   float* const stage1 = smem + wsz + xslots;
 
-  const int b = blockIdx.z;
+  const int b = (int)blockIdx.z - gi * G.batch;
   const int n0 = blockIdx.x * BN;
   const int m0 = blockIdx.y * BM;
   const int tid = threadIdx.x;
@@ -521,32 +537,42 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const vits_conv1d_d
 }
 
 template <int BM, int BN, int WM_, int WN_, int WT, bool V4>
-int launch_tile_v(const vits_conv1d_desc& d, int batch, hipStream_t s, size_t xrs) {
+int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
   constexpr bool BF = WT != VITS_WDT_F32;
-  const size_t wsz = BF ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
-  const size_t xsz = (size_t)d.kc * xrs;
-  if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) || xsz > (size_t)XTile<BN, BF>::floats)
-    return VITS_E_UNSUP;
-  // 32-bit window offsets
-  if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
-    return VITS_E_UNSUP;
-  const size_t xslots = BF ? (xrs * (d.kc + 4) + 1) / 2 : xsz;
-  // + tail pad: the software pipeline reads one k-step past the last chunk
-  const size_t lds = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xrs + 64);
-  dim3 grid((d.n_out + BN - 1) / BN, (d.m + BM - 1) / BM, batch);
+  size_t lds = 0;
+  int gx = 0, gy = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const vits_conv1d_desc& d = g.d[i];
+    const size_t wsz = BF ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
+    const size_t xsz = (size_t)d.kc * xrs[i];
+    if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) || xsz > (size_t)XTile<BN, BF>::floats)
+      return VITS_E_UNSUP;
+    // 32-bit window offsets
+    if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
+      return VITS_E_UNSUP;
+    const size_t xslots = BF ? (xrs[i] * (d.kc + 4) + 1) / 2 : xsz;
+    // + tail pad: the software pipeline reads one k-step past the last chunk
+    const size_t l = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xrs[i] + 64);
+    if (l > lds) lds = l;
+    const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;
+    if (x > gx) gx = x;
+    if (y > gy) gy = y;
+  }
+  dim3 grid(gx, gy, g.n * g.batch);
   dim3 block(256);
+  const vits_conv1d_desc& d = g.d[0];
   switch (d.epi) {
     case VITS_EPI_STORE:
       if (d.split < d.m)
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, WT, V4>), grid, block, lds, s, d);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, WT, V4>), grid, block, lds, s, g);
       else
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, WT, V4>), grid, block, lds, s, d);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, WT, V4>), grid, block, lds, s, g);
       break;
     case VITS_EPI_GATE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, WT, V4>), grid, block, lds, s, d);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, WT, V4>), grid, block, lds, s, g);
       break;
     case VITS_EPI_UPSAMPLE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, WT, V4>), grid, block, lds, s, d);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, WT, V4>), grid, block, lds, s, g);
       break;
     default:
       return VITS_E_UNSUP;
@@ -556,47 +582,67 @@ int launch_tile_v(const vits_conv1d_desc& d, int batch, hipStream_t s, size_t xr
 
 // 16-byte X staging when every window row is a 16-byte-aligned run of time
 // steps (the [B][C][T] activations with T % 4 == 0) and the wider window
-// still fits the stage; element-wise staging otherwise
+// still fits the stage; element-wise staging otherwise.  A group runs one
+// staging kind: mixed members are UNSUP (the caller launches them apart).
 template <int BM, int BN, int WM_, int WN_, int WT>
-int launch_tile(const vits_conv1d_desc& d, int batch, hipStream_t s) {
+int launch_tile(const ConvGroup& g, hipStream_t s) {
   constexpr bool BF = WT != VITS_WDT_F32;
-  const int xw = BN + (d.k - 1) * d.dil;
-  const int xw_pad = (xw + 3) & ~3;
-  const int xsh = (d.pad_left & 3) ? 4 - (d.pad_left & 3) : 0;
-  const int xrs4 = 4 * ((xw + xsh + 3) >> 2);
-  const bool v4 = d.x_tstride == 1 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
-                  (d.tin & 3) == 0 && d.pad_left >= 0 &&
-                  (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
-                  (size_t)d.kc * xrs4 <= (size_t)XTile<BN, BF>::floats;
-  if (v4) return launch_tile_v<BM, BN, WM_, WN_, WT, true>(d, batch, s, xrs4);
-  return launch_tile_v<BM, BN, WM_, WN_, WT, false>(d, batch, s, xw_pad);
+  size_t xrs4[VITS_CONV_GROUP], xrs1[VITS_CONV_GROUP];
+  int nv4 = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const vits_conv1d_desc& d = g.d[i];
+    const int xw = BN + (d.k - 1) * d.dil;
+    xrs1[i] = (xw + 3) & ~3;
+    const int xsh = (d.pad_left & 3) ? 4 - (d.pad_left & 3) : 0;
+    xrs4[i] = 4 * ((xw + xsh + 3) >> 2);
+    const bool v4 = d.x_tstride == 1 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
+                    (d.tin & 3) == 0 && d.pad_left >= 0 &&
+                    (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
+                    (size_t)d.kc * xrs4[i] <= (size_t)XTile<BN, BF>::floats;
+    nv4 += v4;
+  }
+  if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true>(g, s, xrs4);
+  if (nv4 != 0) return VITS_E_UNSUP;
+  return launch_tile_v<BM, BN, WM_, WN_, WT, false>(g, s, xrs1);
 }
 
 template <int WT>
-int conv1d_dispatch(const vits_conv1d_desc& d, int batch, hipStream_t s) {
+int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
   constexpr bool BF = WT != VITS_WDT_F32;
+  const vits_conv1d_desc& d = g.d[0];
+  long blocks = 0;  // whole launch, for the small-grid fallbacks below
+  for (int i = 0; i < g.n; ++i) {
+    const vits_conv1d_desc& e = g.d[i];
+    if (e.tile != d.tile || e.epi != d.epi || (e.split < e.m) != (d.split < d.m) ||
+        e.wdtype != d.wdtype)
+      return VITS_E_UNSUP;
+    const int bm = d.tile == VITS_TILE_128x128 ? 128 : d.tile == VITS_TILE_32x256 ? 32 : 64;
+    const int bn = d.tile == VITS_TILE_64x256 || d.tile == VITS_TILE_32x256 ? 256 : 128;
+    blocks += (long)((e.n_out + bn - 1) / bn) * ((e.m + bm - 1) / bm) * g.batch;
+  }
   switch (d.tile) {
     case VITS_TILE_128x128: {
       // a 128x128 grid that cannot fill the chip twice over (256 CUs) runs
       // as 64x128 tiles: same packing (its W/X budgets are a subset), twice
       // the workgroups
-      const long blocks = (long)((d.n_out + 127) / 128) * ((d.m + 127) / 128) * batch;
-      if (blocks < 512) return launch_tile<64, 128, 2, 2, WT>(d, batch, s);
-      return launch_tile<128, 128, 2, 2, WT>(d, batch, s);
+      if (blocks < 512) return launch_tile<64, 128, 2, 2, WT>(g, s);
+      return launch_tile<128, 128, 2, 2, WT>(g, s);
     }
     case VITS_TILE_64x128:
-      return launch_tile<64, 128, 2, 2, WT>(d, batch, s);
+      return launch_tile<64, 128, 2, 2, WT>(g, s);
     case VITS_TILE_64x256: {
       // same fallback for 64x256 grids (the flow / text-side convs at
       // T ~ 500) when the chunk's input window also fits the 128-column tile
-      const long blocks = (long)((d.n_out + 255) / 256) * ((d.m + 63) / 64) * batch;
-      const int xw_pad128 = (128 + (d.k - 1) * d.dil + 3) & ~3;
-      if (blocks < 512 && d.kc * xw_pad128 <= XTile<128, BF>::floats)
-        return launch_tile<64, 128, 2, 2, WT>(d, batch, s);
-      return launch_tile<64, 256, 1, 4, WT>(d, batch, s);
+      bool fits128 = true;
+      for (int i = 0; i < g.n; ++i) {
+        const int xw_pad128 = (128 + (g.d[i].k - 1) * g.d[i].dil + 3) & ~3;
+        fits128 = fits128 && g.d[i].kc * xw_pad128 <= XTile<128, BF>::floats;
+      }
+      if (blocks < 512 && fits128) return launch_tile<64, 128, 2, 2, WT>(g, s);
+      return launch_tile<64, 256, 1, 4, WT>(g, s);
     }
     case VITS_TILE_32x256:
-      return launch_tile<32, 256, 1, 4, WT>(d, batch, s);
+      return launch_tile<32, 256, 1, 4, WT>(g, s);
     default:
       return VITS_E_UNSUP;
   }
@@ -605,6 +651,6 @@ int conv1d_dispatch(const vits_conv1d_desc& d, int batch, hipStream_t s) {
 }  // namespace vits_conv
 
 // per-type entry points (defined in conv1d_{f32,bf16,f16}.hip)
-int vits_conv1d_dispatch_f32(const vits_conv1d_desc& d, int batch, hipStream_t s);
-int vits_conv1d_dispatch_bf16(const vits_conv1d_desc& d, int batch, hipStream_t s);
-int vits_conv1d_dispatch_f16(const vits_conv1d_desc& d, int batch, hipStream_t s);
+int vits_conv1d_dispatch_f32(const vits_conv::ConvGroup& g, hipStream_t s);
+int vits_conv1d_dispatch_bf16(const vits_conv::ConvGroup& g, hipStream_t s);
+int vits_conv1d_dispatch_f16(const vits_conv::ConvGroup& g, hipStream_t s);

@@ -22,6 +22,8 @@ them; per-call intermediates come from the torch caching allocator.
 """
 from __future__ import annotations
 
+import os
+
 import math
 from typing import Optional
 
@@ -107,6 +109,14 @@ def _conv_eff(conv: torch.nn.Module):
 # ---------------------------------------------------------------------------
 # Generator (HiFi-GAN style decoder with gated ResBlock2)
 # ---------------------------------------------------------------------------
+# grouped launches of the ResBlock2 branches (VITS_GROUP_BRANCHES=0: one
+# launch per conv, for A/B timing)
+_GROUP_BRANCHES = os.environ.get("VITS_GROUP_BRANCHES", "1") != "0"
+# fused ResBlock2 pairs on the 32/64-channel stages (VITS_FUSED_PAIRS=0: the
+# two-conv path, for A/B timing and the parity test of both)
+_FUSED_PAIRS = os.environ.get("VITS_FUSED_PAIRS", "1") != "0"
+
+
 class GeneratorPlan:
     def __init__(self, gen):
         self.signature = None
@@ -156,26 +166,69 @@ class GeneratorPlan:
             xu = ops.conv1d(h, up, in_slope=0.1)
             C, T = xu.shape[1], xu.shape[2]
             xs = torch.empty(B, C, T, device=dev, dtype=torch.float32)
-            tmp = [torch.empty_like(xs), torch.empty_like(xs)]
-            gbuf = torch.empty(B, C // 2, T, device=dev, dtype=torch.float32)
-            descs = []
-            nk = len(blocks)
-            for j, pairs in enumerate(blocks):
-                cur = xu
-                for p, (c1, c2, coff) in enumerate(pairs):
-                    descs.append(make_desc(c1, cur, make_out(gbuf), in_slope=0.1, cond=cond,
-                                           cond_offset=coff))
-                    if p < len(pairs) - 1:
-                        dst = tmp[p & 1]
-                        descs.append(make_desc(c2, gbuf, make_out(dst, res=cur)))
-                        cur = dst
-                    else:
-                        descs.append(make_desc(c2, gbuf, make_out(
-                            xs, res=cur, accumulate=j > 0,
-                            post_div=float(nk) if j == nk - 1 else 1.0)))
-            ops.conv1d_launch_seq(descs, B, dev)
+            self._run_stage(blocks, xu, xs, cond, B, dev)
             h = xs
         return ops.conv_post_tanh(h, self.post_w, out=out)
+
+    @staticmethod
+    def _run_stage(blocks, xu, xs, cond, B, dev):
+        """The nk ResBlock2 branches of one stage (models.py:311-313) on xu,
+        their mean into xs.  Branches are independent until the mean: each
+        keeps its own buffers, and the work of one dilation index of all
+        branches shares launches - fused pairs (csrc/resblock.hip, where
+        ops.resblock_pair_supported) as one launch, the other branches' c1
+        (gate epilogue) and c2 (residual epilogue) convs as one grouped
+        launch each.  The last pairs accumulate the mean into xs in branch
+        order (separate launches)."""
+        nk = len(blocks)
+        npairs = len(blocks[0])
+        if any(len(pairs) != npairs for pairs in blocks):
+            raise NotImplementedError("ResBlock2 branches with different dilation counts")
+        C, T = xu.shape[1], xu.shape[2]
+        fused = [[_FUSED_PAIRS and ops.resblock_pair_supported(pr[0], pr[1], T) for pr in pairs]
+                 for pairs in blocks]
+        tmp = [[torch.empty_like(xs), torch.empty_like(xs)] for _ in range(nk)]
+        gbuf = [None if all(fused[j]) else
+                torch.empty(B, C // 2, T, device=dev, dtype=torch.float32) for j in range(nk)]
+        cur = [xu] * nk
+
+        def c1_desc(j, p):
+            return make_desc(blocks[j][p][0], cur[j], make_out(gbuf[j]), in_slope=0.1, cond=cond,
+                             cond_offset=blocks[j][p][2])
+
+        def grouped(ds):
+            return [tuple(ds)] if _GROUP_BRANCHES else list(ds)
+
+        for p in range(npairs):
+            fj = [j for j in range(nk) if fused[j][p]]
+            cj = [j for j in range(nk) if not fused[j][p]]
+            if p < npairs - 1:
+                dst = [tmp[j][p & 1] for j in range(nk)]
+                if fj:
+                    ops.resblock_pair_launch(tuple(
+                        ops.resblock_pair_desc(blocks[j][p][0], blocks[j][p][1], cur[j], dst[j],
+                                               cond=cond, cond_offset=blocks[j][p][2])
+                        for j in fj), B, dev)
+                if cj:
+                    descs = grouped(c1_desc(j, p) for j in cj)
+                    descs += grouped(make_desc(blocks[j][p][1], gbuf[j],
+                                               make_out(dst[j], res=cur[j])) for j in cj)
+                    ops.conv1d_launch_seq(descs, B, dev)
+                cur = dst
+                continue
+            # last pair of every branch: accumulate the mean, in branch order
+            descs = grouped(c1_desc(j, p) for j in cj)
+            if descs:
+                ops.conv1d_launch_seq(descs, B, dev)
+            for j in range(nk):
+                kw = dict(accumulate=j > 0, post_div=float(nk) if j == nk - 1 else 1.0)
+                if fused[j][p]:
+                    ops.resblock_pair_launch(ops.resblock_pair_desc(
+                        blocks[j][p][0], blocks[j][p][1], cur[j], xs, cond=cond,
+                        cond_offset=blocks[j][p][2], **kw), B, dev)
+                else:
+                    ops.conv1d_launch_seq([make_desc(blocks[j][p][1], gbuf[j],
+                                                     make_out(xs, res=cur[j], **kw))], B, dev)
 
 
 # ---------------------------------------------------------------------------

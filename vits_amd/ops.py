@@ -17,6 +17,7 @@ import torch
 
 from . import _lib
 from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
+                   ResblockPairDesc,
                    EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS,
                    check)
 
@@ -358,14 +359,29 @@ class ConvTimer:
         return False
 
     def launch(self, lib, desc, batch, device):
+        """One launch: a ConvDesc, or a tuple of ConvDescs run as one grid."""
+        group = tuple(desc) if isinstance(desc, (tuple, list)) else (desc,)
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         stream = torch.cuda.current_stream(device)
         s.record(stream)
-        check(lib.vits_conv1d_forward(C.byref(desc), batch, stream.cuda_stream),
-              "vits_conv1d_forward")
+        arr = (ConvDesc * len(group))(*group)
+        sizes = (C.c_int32 * 1)(len(group))
+        check(lib.vits_conv1d_forward_groups(arr, sizes, 1, batch, stream.cuda_stream),
+              "vits_conv1d_forward_groups")
         e.record(stream)
-        self.records.append((s, e, conv_flops(desc, batch)))
+        self.records.append((s, e, sum(conv_flops(d, batch) for d in group)))
+
+    def launch_pairs(self, lib, group, batch, device):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        stream = torch.cuda.current_stream(device)
+        s.record(stream)
+        arr = (ResblockPairDesc * len(group))(*group)
+        check(lib.vits_resblock_pair_forward(arr, len(group), batch, stream.cuda_stream),
+              "vits_resblock_pair_forward")
+        e.record(stream)
+        self.records.append((s, e, sum(resblock_pair_flops(d, batch) for d in group)))
 
     def summary(self):
         torch.cuda.synchronize()
@@ -373,6 +389,79 @@ class ConvTimer:
         fl = [f for _, _, f in self.records]
         return dict(launches=len(ms), total_ms=float(sum(ms)), total_flops=int(sum(fl)),
                     avg_ms=float(sum(ms) / max(1, len(ms))))
+
+
+# ---------------------------------------------------------------------------
+# fused ResBlock2 pair (csrc/resblock.hip)
+# ---------------------------------------------------------------------------
+_RB_KC = {}
+
+
+RESBLOCK_PAIR_MAX_K = 7
+
+
+def resblock_pair_supported(c1: PackedConv, c2: PackedConv, T: int) -> bool:
+    """Pairs that run fused (csrc/resblock.hip): the fp32 32- and 64-channel
+    stages (C' = C, 16-byte aligned time rows) with k <= 7.  tools/rb_bench.py
+    on MI355X (B=16, Ty=500): fused vs the two-conv path k=3 +6..11 %, k=7
+    +0..10 %, k=11 -4..-8 % (the c1 phase recomputes the c2 halo and the
+    workgroup holds the gated tile in LDS: two workgroups per CU instead of
+    three) - so k=11 pairs keep the two-conv path."""
+    C = c2.out_channels
+    return (c1.wdtype == WDT_F32 and c2.wdtype == WDT_F32 and C in (32, 64)
+            and c1.m == C and c1.cin == C and c2.cin == C // 2 and c1.k == c2.k
+            and c1.k <= RESBLOCK_PAIR_MAX_K and c2.dil == 1 and T % 4 == 0
+            and _resblock_kc(C, c1.k, c1.dil) is not None)
+
+
+def _resblock_kc(ch: int, k: int, dil: int):
+    key = (ch, k, dil)
+    if key not in _RB_KC:
+        kc1, kc2 = C.c_int(), C.c_int()
+        rc = _lib.load().vits_resblock_pair_kc(ch, k, dil, kc1, kc2)
+        _RB_KC[key] = (kc1.value, kc2.value) if rc == 0 else None
+    return _RB_KC[key]
+
+
+def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch.Tensor, *,
+                       cond: Optional[torch.Tensor] = None, cond_offset: int = 0,
+                       in_slope: float = 0.1, accumulate: bool = False,
+                       post_div: float = 1.0) -> ResblockPairDesc:
+    """y = x + c2(gate(c1(lrelu(x)) + cond)) in one launch (modules.py:250-260)."""
+    assert x.dtype == torch.float32 and y.dtype == torch.float32 and x.stride(2) == 1
+    C_, T = x.shape[1], x.shape[2]
+    kc1, kc2 = _resblock_kc(C_, c1.k, c1.dil)
+    d = ResblockPairDesc()
+    d.x, d.x_bstride, d.x_cstride, d.t_len = x.data_ptr(), x.stride(0), x.stride(1), T
+    d.channels, d.in_slope = C_, in_slope
+    d.w1, d.m_pad1, d.cin_pad1, d.kc1 = c1.w.data_ptr(), c1.m_pad, c1.cin_pad, kc1
+    d.k, d.dil, d.kc2 = c1.k, c1.dil, kc2
+    d.b1 = _ptr(c1.bias)
+    if cond is not None:
+        d.cond, d.cond_bstride = cond.data_ptr() + 4 * cond_offset, cond.stride(0)
+    d.w2, d.m_pad2, d.cin_pad2 = c2.w.data_ptr(), c2.m_pad, c2.cin_pad
+    d.b2 = _ptr(c2.bias)
+    d.y, d.y_bstride, d.y_cstride = y.data_ptr(), y.stride(0), y.stride(1)
+    d.accumulate, d.post_div = int(accumulate), float(post_div)
+    return d
+
+
+def resblock_pair_flops(d: ResblockPairDesc, batch: int) -> int:
+    """Algorithmic FLOPs of the pair (c1 + c2 as the reference computes
+    them; the kernel's recomputed halo columns are not counted)."""
+    C_, k, T = d.channels, d.k, d.t_len
+    return 2 * batch * T * (C_ * C_ * k + (C_ // 2) * C_ * k)
+
+
+def resblock_pair_launch(descs, batch: int, device: torch.device):
+    """One launch of up to 3 independent pairs (tuple) or one pair."""
+    group = tuple(descs) if isinstance(descs, (tuple, list)) else (descs,)
+    lib = _lib.load()
+    if ConvTimer.active is not None:
+        return ConvTimer.active.launch_pairs(lib, group, batch, device)
+    arr = (ResblockPairDesc * len(group))(*group)
+    check(lib.vits_resblock_pair_forward(arr, len(group), batch, _stream_ptr(device)),
+          "vits_resblock_pair_forward")
 
 
 def conv1d_launch(desc: ConvDesc, batch: int, device: torch.device):
@@ -383,14 +472,23 @@ def conv1d_launch(desc: ConvDesc, batch: int, device: torch.device):
 
 
 def conv1d_launch_seq(descs, batch: int, device: torch.device):
+    """Run descriptors in order, one host call.  An item may be a tuple of
+    independent ConvDescs (the ResBlock2 branches of one Generator stage):
+    they share one launch (vits_conv1d_forward_groups)."""
     lib = _lib.load()
     if ConvTimer.active is not None:
         for d in descs:
             ConvTimer.active.launch(lib, d, batch, device)
         return
-    arr = (ConvDesc * len(descs))(*descs)
-    check(lib.vits_conv1d_forward_seq(arr, len(descs), batch, _stream_ptr(device)),
-          "vits_conv1d_forward_seq")
+    flat, sizes = [], []
+    for d in descs:
+        group = tuple(d) if isinstance(d, (tuple, list)) else (d,)
+        flat.extend(group)
+        sizes.append(len(group))
+    arr = (ConvDesc * len(flat))(*flat)
+    sz = (C.c_int32 * len(sizes))(*sizes)
+    check(lib.vits_conv1d_forward_groups(arr, sz, len(sizes), batch, _stream_ptr(device)),
+          "vits_conv1d_forward_groups")
 
 
 def conv1d(x: torch.Tensor, layer: PackedConv, *, in_slope: float = 1.0, act: int = ACT_NONE,
