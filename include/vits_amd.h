@@ -236,7 +236,10 @@ int64_t vits_stft_workspace(int batch, int length, int n_fft, int hop, int pad);
 /* MR-STFT loss, stft_loss.py:47-95): up to 16 jobs, each with its own    */
 /* signal batch, resolution and outputs.  Forward uses x, window, sizes,  */
 /* eps, mag, re, im; backward uses grad_mag, mag, re, im, window, sizes,  */
-/* grad_x and a workspace of vits_stft_workspace_multi floats.            */
+/* grad_x and a workspace of vits_stft_workspace_multi floats.  layout 1: */
+/* mag / re / im / grad_mag are [B][frames][n_fft/2+1] (frame-major: a    */
+/* workgroup's frames are one contiguous run - coalesced stores); 0: the  */
+/* torch.stft layout [B][n_fft/2+1][frames].                              */
 typedef struct vits_stft_job {
   const float* x;
   const float* window;
@@ -252,7 +255,7 @@ typedef struct vits_stft_job {
   int32_t win;
   int32_t pad;
   float eps;
-  int32_t reserved;
+  int32_t layout;
 } vits_stft_job;
 int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs, void* stream);
 int vits_stft_mag_backward_multi(const vits_stft_job* jobs, int njobs, float* workspace,

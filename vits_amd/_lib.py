@@ -130,7 +130,7 @@ class StftJob(C.Structure):
         ("win", C.c_int32),
         ("pad", C.c_int32),
         ("eps", C.c_float),
-        ("reserved", C.c_int32),
+        ("layout", C.c_int32),
     ]
 
 

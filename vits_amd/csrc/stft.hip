@@ -204,6 +204,7 @@ struct StftJobD {
   float* gx;            // backward output [B][L]
   int L, n, log2n, hop, win, pad, frames, fpb, batch;
   float eps;
+  int fmajor;  // mag / re / im / grad_mag as [B][frames][n/2+1] (else [B][n/2+1][frames])
 };
 
 // forward: frames f0 .. f0+fpb-1 of utterance b (radix-4 Stockham, fft_lds4;
@@ -240,6 +241,20 @@ __device__ void stft_fwd_block(const StftJobD& J, int fblk, int b, float2* sfft)
   __syncthreads();
   const float2* out = fft_lds4(a, bbuf, tw, n, J.log2n, fpb, -1.f);
   const int nb = n / 2 + 1;
+  if (J.fmajor) {
+    // frame-major: the workgroup's fpb frames are one contiguous run of
+    // fpb * nb outputs - every store instruction writes whole lines
+    const int nf = min(fpb, J.frames - f0);
+    const int64_t base = ((int64_t)b * J.frames + f0) * nb;
+    for (int i = threadIdx.x; i < nf * nb; i += blockDim.x) {
+      const int f = i / nb;
+      const float2 c = out[f * n + (i - f * nb)];
+      J.mag[base + i] = sqrtf(c.x * c.x + c.y * c.y + J.eps);
+      if (J.re) J.re[base + i] = c.x;
+      if (J.im) J.im[base + i] = c.y;
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < fpb * nb; i += blockDim.x) {
     const int k = i / fpb;
     const int f = i - k * fpb;
@@ -268,11 +283,21 @@ __device__ void stft_bwd_frames_block(const StftJobD& J, int fblk, int b, float2
 #pragma unroll
   for (int q = 0; q < STFT_PER; ++q) {
     const int i = threadIdx.x + q * STFT_WG;
-    const int k = i / fpb;  // bin-major so reads along frames are contiguous
-    const int f = i - k * fpb;
+    // element (bin k, frame f) of this thread: ordered so the reads run along
+    // the contiguous axis of the layout (frames, or bins when frame-major)
+    int k, f;
+    if (J.fmajor) {
+      f = i / n;
+      k = i - f * n;
+    } else {
+      k = i / fpb;
+      f = i - k * fpb;
+    }
     const int fr = f0 + f;
     const bool ok = i < fpb * n && k < nb && fr < J.frames;
-    const int64_t o = ok ? ((int64_t)b * nb + k) * J.frames + fr : 0;
+    const int64_t o = !ok ? 0
+                      : J.fmajor ? ((int64_t)b * J.frames + fr) * nb + k
+                                 : ((int64_t)b * nb + k) * J.frames + fr;
     gm[q] = ok ? J.gmag[o] : 0.f;
     mg[q] = ok ? J.mag[o] : 1.f;
     rr[q] = ok ? J.re[o] : 0.f;
@@ -282,8 +307,14 @@ __device__ void stft_bwd_frames_block(const StftJobD& J, int fblk, int b, float2
   for (int q = 0; q < STFT_PER; ++q) {
     const int i = threadIdx.x + q * STFT_WG;
     if (i < fpb * n) {
-      const int k = i / fpb;
-      const int f = i - k * fpb;
+      int k, f;
+      if (J.fmajor) {
+        f = i / n;
+        k = i - f * n;
+      } else {
+        k = i / fpb;
+        f = i - k * fpb;
+      }
       const float sc = gm[q] / mg[q];
       a[f * n + k] = make_float2(sc * rr[q], sc * ii[q]);
     }
@@ -485,6 +516,7 @@ extern "C" int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs,
     M.job[i].mag = q.mag;
     M.job[i].re = q.re;
     M.job[i].im = q.im;
+    M.job[i].fmajor = q.layout;
     M.per_b[i] = job_fblocks(M.job[i]);
     blocks += M.per_b[i] * q.batch;
     M.end[i] = blocks;
@@ -526,6 +558,7 @@ extern "C" int vits_stft_mag_backward_multi(const vits_stft_job* jobs, int njobs
     J.im = q.im;
     J.dframes = workspace + woff;
     J.gx = q.grad_x;
+    J.fmajor = q.layout;
     woff += vits_stft_workspace(q.batch, q.length, q.n_fft, q.hop, q.pad);
     F.job[i] = J;
     M.per_b[i] = job_fblocks(J);

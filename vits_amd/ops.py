@@ -734,7 +734,9 @@ class _StftMagMulti(torch.autograd.Function):
             window = window.contiguous().float()
             B, L = x.shape
             frames = (L + 2 * pad - n_fft) // hop + 1
-            mag = torch.empty(B, n_fft // 2 + 1, frames, device=x.device, dtype=torch.float32)
+            # frame-major storage (coalesced kernel stores, layout 1); the
+            # caller gets the [B, n_fft/2+1, frames] view torch.stft returns
+            mag = torch.empty(B, frames, n_fft // 2 + 1, device=x.device, dtype=torch.float32)
             need = ctx.needs_input_grad[i + 1]
             re = torch.empty_like(mag) if need else None
             im = torch.empty_like(mag) if need else None
@@ -742,8 +744,9 @@ class _StftMagMulti(torch.autograd.Function):
             j.x, j.window, j.mag, j.re, j.im = x.data_ptr(), window.data_ptr(), mag.data_ptr(), \
                 _ptr(re), _ptr(im)
             j.batch, j.length, j.n_fft, j.hop, j.win, j.pad, j.eps = B, L, n_fft, hop, win, pad, eps
+            j.layout = 1
             keep += [x, window]
-            mags.append(mag)
+            mags.append(mag.transpose(1, 2))
             saved.append((mag, re, im, window, B, L, n_fft, hop, win, pad) if need else None)
         check(_lib.load().vits_stft_mag_forward_multi(jobs, len(xs), _stream_ptr(xs[0].device)),
               "vits_stft_mag_forward_multi")
@@ -767,12 +770,15 @@ class _StftMagMulti(torch.autograd.Function):
         for q, i in enumerate(idx):
             mag, re, im, window, B, L, n_fft, hop, win, pad = ctx.saved[i]
             g = gmags[i]
-            g = torch.zeros_like(mag) if g is None else g.contiguous().float()
+            # frame-major like the saved forward outputs (free when the
+            # gradient is itself a transposed view of frame-major storage)
+            g = torch.zeros_like(mag) if g is None else g.transpose(1, 2).contiguous().float()
             gx = torch.empty(B, L, device=ctx.dev, dtype=torch.float32)
             j = jobs[q]
             j.grad_mag, j.mag, j.re, j.im, j.window, j.grad_x = g.data_ptr(), mag.data_ptr(), \
                 re.data_ptr(), im.data_ptr(), window.data_ptr(), gx.data_ptr()
             j.batch, j.length, j.n_fft, j.hop, j.win, j.pad = B, L, n_fft, hop, win, pad
+            j.layout = 1
             keep.append(g)
             grads[i] = gx
         lib = _lib.load()
