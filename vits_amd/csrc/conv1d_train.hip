@@ -75,7 +75,12 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 // stores into ws[split][k][cout][cin] (+ bias partials ws_b[split][cout]);
 // wgrad_reduce_kernel then sums the splits.  Otherwise fp32 atomics into
 // p.dw_t / p.dbias.
-template <int NK, int WT, bool PARTIAL>
+// VEC: 16-byte staging loads (the [B][C][T] tensors with 16-byte aligned
+// rows and tin % 4 == 0): dY as 4 consecutive steps of one row, X as 4
+// consecutive steps of a channel pair from a 4-aligned window start (sh
+// rows of shift, read back with the same shift) - a quarter of the load
+// instructions of the element-wise map.
+template <int NK, int WT, bool PARTIAL, bool VEC>
 __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_conv1d_wgrad_desc p,
                                                                      int tchunks, int total_chunks,
                                                                      int chunks_per_wg,
@@ -118,6 +123,80 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
   // time steps of one channel row (256 B).
   float dyv[16];
   float xv[32];
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  // VEC window: rows from the 4-aligned start t0 - pad_left - sh
+  const int sh = VEC ? ((p.pad_left & 3) ? 4 - (p.pad_left & 3) : 0) : 0;
+
+  auto gload_vec = [&](int chunk) {
+    const int b = chunk / tchunks;
+    const int t0 = (chunk - b * tchunks) * KT;
+    const float* dyb = p.dy + (int64_t)b * p.dy_bstride;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const int co = m0 + (u >> 4);
+      const int t = t0 + 4 * (u & 15);
+      const float* src = dyb + (int64_t)co * p.dy_cstride + t;
+      f32x4v v = {0.f, 0.f, 0.f, 0.f};
+      if (co < p.cout) {
+        if (t + 3 < p.n_out) {
+          v = *reinterpret_cast<const f32x4v*>(src);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = t + e < p.n_out ? src[e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dyv[4 * q + e] = v[e];
+    }
+    const float* xb = p.x + (int64_t)b * p.x_bstride;
+    const int ts = t0 - p.pad_left - sh;  // multiple of 4
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const int ci = c0 + 2 * (u >> 5);
+      const int r4 = 4 * (u & 31);
+      const int t = ts + r4;
+      const bool tok = r4 < wr + sh && t >= 0 && t < p.tin;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        f32x4v v = {0.f, 0.f, 0.f, 0.f};
+        if (tok && ci + e < p.cin)
+          v = *reinterpret_cast<const f32x4v*>(xb + (int64_t)(ci + e) * p.x_cstride + t);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xv[8 * q + 4 * e + i] = v[i];
+      }
+    }
+  };
+  auto lstore_vec = [&](uint16_t* st) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const float a0 = dyv[4 * q], a1 = dyv[4 * q + 1], a2 = dyv[4 * q + 2], a3 = dyv[4 * q + 3];
+      if (do_bias) bsum[q] += (a0 + a1) + (a2 + a3);
+      uint32_t* d = reinterpret_cast<uint32_t*>(st + (u >> 4) * DY_LD + 4 * (u & 15));
+      d[0] = pack2<WT>(a0, a1);
+      d[1] = pack2<WT>(a2, a3);
+    }
+    uint32_t* xl = reinterpret_cast<uint32_t*>(st + DY_HALVES);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const int cl = 2 * (u >> 5);
+      const int r4 = 4 * (u & 31);
+      if (r4 < wr + sh) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v0 = xv[8 * q + i], v1 = xv[8 * q + 4 + i];
+          if (act_in) {
+            v0 = v0 < 0.f ? v0 * slope : v0;
+            v1 = v1 < 0.f ? v1 * slope : v1;
+          }
+          xl[((r4 + i) * X_LD + cl) >> 1] = pack2<WT>(v0, v1);
+        }
+      }
+    }
+  };
 
   auto gload = [&](int chunk) {
     const int b = chunk / tchunks;
@@ -183,11 +262,16 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
   const int qq = (lane >> 2) & 3;
   const int pp = lane & 3;
   const int a_off = (wm + l32) * DY_LD + 8 * lhi;
-  const int b_off = DY_HALVES + (8 * (g >> 1) + qq) * X_LD + wn + 16 * (g & 1) + 4 * pp;
+  const int b_off = DY_HALVES + (8 * (g >> 1) + qq + sh) * X_LD + wn + 16 * (g & 1) + 4 * pp;
 
   if (ch_begin < ch_end) {
-    gload(ch_begin);
-    lstore(lds);
+    if constexpr (VEC) {
+      gload_vec(ch_begin);
+      lstore_vec(lds);
+    } else {
+      gload(ch_begin);
+      lstore(lds);
+    }
   }
   __syncthreads();
   for (int ch = ch_begin; ch < ch_end; ++ch) {
@@ -195,7 +279,12 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
     uint16_t* cur = lds + (it & 1) * STAGE_HALVES;
     uint16_t* nxt = lds + ((it + 1) & 1) * STAGE_HALVES;
     const bool more = ch + 1 < ch_end;
-    if (more) gload(ch + 1);
+    if (more) {
+      if constexpr (VEC)
+        gload_vec(ch + 1);
+      else
+        gload(ch + 1);
+    }
 #pragma unroll
     for (int s = 0; s < KT / 16; ++s) {
       const V8 a = *reinterpret_cast<const V8*>(cur + a_off + 16 * s);
@@ -213,7 +302,12 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
           acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc[j], 0, 0, 0);
       }
     }
-    if (more) lstore(nxt);
+    if (more) {
+      if constexpr (VEC)
+        lstore_vec(nxt);
+      else
+        lstore(nxt);
+    }
     __syncthreads();
   }
 
@@ -234,7 +328,22 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
       }
     }
   }
-  if (do_bias) {
+  if (do_bias && VEC) {
+    // VEC map: row (tid >> 4) + 16 q is shared by 16 consecutive lanes
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = bsum[q];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+      const int co = m0 + (tid >> 4) + 16 * q;
+      if ((tid & 15) == 0 && co < p.cout) {
+        if constexpr (PARTIAL)
+          ws_b[(int64_t)blockIdx.x * p.cout + co] = v;
+        else
+          unsafeAtomicAdd(p.dbias + co, v);
+      }
+    }
+  } else if (do_bias) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       float v = bsum[q];
@@ -340,11 +449,22 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
   const int tchunks = w.tchunks, total = w.total, cpw = w.cpw;
   dim3 grid(w.splits, (d.cin + WG_N - 1) / WG_N, (d.cout + WG_M - 1) / WG_M);
   const size_t lds = 2 * STAGE_HALVES * sizeof(uint16_t);
+  const int sh = (d.pad_left & 3) ? 4 - (d.pad_left & 3) : 0;
+  const bool vec = (d.dy_cstride & 3) == 0 && (d.dy_bstride & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(d.dy) & 15) == 0 && (d.x_cstride & 3) == 0 &&
+                   (d.x_bstride & 3) == 0 && (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
+                   (d.tin & 3) == 0 && KT + (d.k - 1) * d.dil + sh <= MAX_WR &&
+                   d.k > 1;  // k = 1 (tools/wgrad_split_bench.py: 40 -> 53 us) keeps the
+                             // element-wise map: half the VEC units idle at a 64-row window
   switch (d.k) {
-#define VITS_WG_CASE(NK) \
-  case NK:               \
-    hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL>), grid, dim3(256), lds, s, d, tchunks, total, \
-                       cpw, ws, ws_b);                                                            \
+#define VITS_WG_CASE(NK)                                                                           \
+  case NK:                                                                                         \
+    if (vec)                                                                                       \
+      hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL, true>), grid, dim3(256), lds, s, d,        \
+                         tchunks, total, cpw, ws, ws_b);                                           \
+    else                                                                                           \
+      hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL, false>), grid, dim3(256), lds, s, d,       \
+                         tchunks, total, cpw, ws, ws_b);                                           \
     break;
     VITS_WG_CASE(1)
     VITS_WG_CASE(2)
