@@ -132,6 +132,11 @@ typedef struct vits_conv1d_desc {
   int64_t gmask_bstride;
   int32_t gmask_cstride;
   float gmask_slope;
+  /* io16 != 0 (16-bit wdtype only): x, out0/out1 y and res, and gmask are  */
+  /* tensors of the 16-bit operand type (strides in elements); fp32 I/O    */
+  /* otherwise.  The fp16-autocast training convs keep fp16 activations.   */
+  int32_t io16;
+  int32_t reserved;
 } vits_conv1d_desc;
 
 #define VITS_WDT_F32 0
@@ -332,6 +337,10 @@ typedef struct vits_conv1d_wgrad_desc {
   int32_t wdtype;         /* MFMA operand type: VITS_WDT_F16 / VITS_WDT_BF16 */
   int32_t reserved;       /* > 0: (b, t)-chunks of 64 steps per workgroup    */
                           /* (tuning override), 0 = automatic                */
+  int32_t io16;           /* dy / x are tensors of the 16-bit operand type   */
+                          /* (strides in elements; 8-byte aligned rows,      */
+                          /* tin % 4 == 0, else VITS_E_UNSUP)                */
+  int32_t reserved2;
 } vits_conv1d_wgrad_desc;
 /* dW[co][ci][j] = sum_{b,t} dY[b][co][t] * act(x[b][ci][t - pad_left + j*dil]) */
 /* (operands rounded to wdtype, fp32 accumulation; VITS_E_UNSUP when       */
@@ -359,6 +368,17 @@ int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t dy_cstride, 
                        int64_t x_bstride, int32_t x_cstride, const float* g, int64_t g_bstride,
                        float* dx, int64_t dx_bstride, int32_t dx_cstride, float* dg, int batch,
                        int half_channels, int t_len, void* stream);
+/* The same with x / g / y (and dy / x / g / dx) of the 16-bit type wdtype */
+/* (VITS_WDT_F16 / _BF16: the fp16 activations of the autocast training    */
+/* step), fp32 math, dg fp32.                                              */
+int vits_gate_forward_io16(const void* x, int64_t x_bstride, int32_t x_cstride, const void* g,
+                           int64_t g_bstride, void* y, int64_t y_bstride, int32_t y_cstride,
+                           int batch, int half_channels, int t_len, int wdtype, void* stream);
+int vits_gate_backward_io16(const void* dy, int64_t dy_bstride, int32_t dy_cstride, const void* x,
+                            int64_t x_bstride, int32_t x_cstride, const void* g,
+                            int64_t g_bstride, void* dx, int64_t dx_bstride, int32_t dx_cstride,
+                            float* dg, int batch, int half_channels, int t_len, int wdtype,
+                            void* stream);
 
 /* ---------------------------------------------------------------------- */
 /* One ResBlock2 dilation pair of the Generator as ONE kernel              */

@@ -15,6 +15,11 @@ from vits_amd import train_ops
 pytestmark = pytest.mark.gpu
 
 TOL = 2e-4
+# outputs / input gradients of the 16-bit-activation path (Conv1dHip16,
+# GateHip16: the reference's autocast convs return fp16) are rounded to fp16
+# once more: 2^-11 of each element, within 1.5e-3 of the tensor's max
+TOL16 = 1.5e-3
+TOL_Y = TOL16 if train_ops.TRAIN_IO16 else TOL
 
 
 def _close(a, b, what, tol=TOL):
@@ -47,20 +52,28 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("io16", [False, True])
 @pytest.mark.parametrize("B,cin,cout,k,dil,pad,T,slope", CASES)
-def test_conv1d_train_fwd_bwd(device, B, cin, cout, k, dil, pad, T, slope):
+def test_conv1d_train_fwd_bwd(device, B, cin, cout, k, dil, pad, T, slope, io16):
+    """fp32 activations (Conv1dHip) and fp16 activations (Conv1dHip16: x, y,
+    dY, dX fp16, read / written by the kernels as such)."""
     g = torch.Generator().manual_seed(B * 7919 + cin * 31 + cout + k * 3 + dil)
     x = torch.randn(B, cin, T, generator=g)
     w = torch.randn(cout, cin, k, generator=g) / (cin * k) ** 0.5
     b = torch.randn(cout, generator=g) * 0.1
     T_out = T + 2 * pad - (k - 1) * dil
     dy = torch.randn(B, cout, T_out, generator=g)
+    if io16:  # the fp16 tensors the autocast step hands over
+        x, dy = _r16(x), _r16(dy)
+    fn = train_ops.Conv1dHip16 if io16 else train_ops.Conv1dHip
+    tol = TOL16 if io16 else TOL
 
-    xd = x.to(device).requires_grad_(True)
+    xd = (x.half() if io16 else x).to(device).requires_grad_(True)
     wd = w.to(device).requires_grad_(True)
     bd = b.to(device).requires_grad_(True)
-    y = train_ops.Conv1dHip.apply(xd, wd, bd, dil, pad, slope, train_ops.TRAIN_WDTYPE)
-    y.backward(dy.to(device))
+    y = fn.apply(xd, wd, bd, dil, pad, slope, train_ops.TRAIN_WDTYPE)
+    assert y.dtype == (torch.float16 if io16 else torch.float32)
+    y.backward((dy.half() if io16 else dy).to(device))
 
     xr = _r16(x).requires_grad_(True)
     wr = _r16(w).requires_grad_(True)
@@ -70,10 +83,10 @@ def test_conv1d_train_fwd_bwd(device, B, cin, cout, k, dil, pad, T, slope):
     xa16 = xa + (_r16(xa.detach()) - xa.detach())
     yr = F.conv1d(xa16, wr, br, padding=pad, dilation=dil)
     yr.backward(_r16(dy))
-    _close(y, yr, "y")
-    _close(xd.grad, xr.grad, "dx")
+    _close(y, yr, "y", tol=tol)
+    _close(xd.grad, xr.grad, "dx", tol=tol)
     _close(wd.grad, wr.grad, "dw")
-    # dbias: the kernel sums the unrounded fp32 dY
+    # dbias: the kernel sums the dY it is given in fp32
     _close(bd.grad, dy.sum((0, 2)), "db")
 
 
@@ -88,8 +101,9 @@ def test_conv1d_train_module_helper_matches_torch_module(device):
     x = torch.randn(2, 64, 300)
     with torch.autocast("cuda", dtype=torch.float16):
         y = train_ops.conv1d(conv, x.to(device), in_slope=0.1)
-    assert y.dtype == torch.float32  # the HIP op (a torch autocast conv returns fp16)
-    y.square().sum().backward()
+    # fp16 like a torch autocast conv (the 16-bit-activation path), else fp32
+    assert y.dtype == (torch.float16 if train_ops.TRAIN_IO16 else torch.float32)
+    y.float().square().sum().backward()
     yr = ref(F.leaky_relu(x, 0.1))
     yr.square().sum().backward()
     _close(y, yr, "y", tol=3e-3)   # fp16 operands vs fp32 torch
@@ -106,8 +120,8 @@ def test_conv1d_train_autocast(device):
         h = x * 2.0
         h16 = h.half()
         y = train_ops.conv1d(conv, h16)
-    assert y.dtype == torch.float32
-    y.sum().backward()
+    assert y.dtype == (torch.float16 if train_ops.TRAIN_IO16 else torch.float32)
+    y.float().sum().backward()
     assert x.grad is not None and torch.isfinite(x.grad).all()
     assert conv.weight.grad is not None and conv.bias.grad is not None
 
@@ -175,6 +189,30 @@ def test_gate_fwd_bwd(device, B, H, T, with_g):
         _close(gd.grad, gr.grad, "dg", tol=1e-5)
 
 
+@pytest.mark.parametrize("B,H,T,with_g", [(2, 256, 500, True), (3, 16, 1537, True), (2, 64, 77, False)])
+def test_gate_fwd_bwd_io16(device, B, H, T, with_g):
+    """GateHip16 (x, g, y, dY, dX fp16; fp32 math, the cond gradient summed
+    in fp32) against torch autograd in fp32 on the same fp16 inputs."""
+    gen = torch.Generator().manual_seed(H + T + 1)
+    x = _r16(torch.randn(B, 2 * H, T, generator=gen))
+    g = _r16(torch.randn(B, 2 * H, generator=gen)) if with_g else None
+    dy = _r16(torch.randn(B, H, T, generator=gen))
+    xd = x.half().to(device).requires_grad_(True)
+    gd = g.half().to(device).requires_grad_(True) if with_g else None
+    y = train_ops.GateHip16.apply(xd, gd, train_ops.TRAIN_WDTYPE)
+    assert y.dtype == torch.float16
+    y.backward(dy.half().to(device))
+    xr = x.clone().requires_grad_(True)
+    gr = g.clone().requires_grad_(True) if with_g else None
+    xx = xr + gr.unsqueeze(-1) if with_g else xr
+    yr = torch.tanh(xx[:, :H]) * torch.sigmoid(xx[:, H:])
+    yr.backward(dy)
+    _close(y, yr, "y", tol=TOL16)
+    _close(xd.grad, xr.grad, "dx", tol=TOL16)
+    if with_g:
+        _close(gd.grad, gr.grad, "dg", tol=2 * TOL16)
+
+
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("B,cin,cout,k,dil,pad,T,slope", [
     (2, 256, 512, 5, 1, 2, 500, 1.0),      # large weight (atomic by default)
@@ -220,8 +258,9 @@ def test_conv_transpose1d_train_polyphase(device, C, O, K, u, T):
     xd = x.to(device).requires_grad_(True)
     with torch.autocast("cuda", dtype=torch.float16):
         y = train_ops.conv_transpose1d(md, xd, in_slope=0.1)
-    assert y.dtype == torch.float32 and y.shape == (2, O, T * u)
-    y.backward(dy.to(device))
+    assert y.dtype == (torch.float16 if train_ops.TRAIN_IO16 else torch.float32)
+    assert y.shape == (2, O, T * u)
+    y.backward(dy.to(device).to(y.dtype))
 
     w = torch._weight_norm(m.weight_v.detach().cpu(), m.weight_g.detach().cpu(), 0)
     wr = _r16(w).requires_grad_(True)
@@ -231,15 +270,15 @@ def test_conv_transpose1d_train_polyphase(device, C, O, K, u, T):
     xa16 = xa + (_r16(xa.detach()) - xa.detach())
     yr = F.conv_transpose1d(xa16, wr, br, stride=u, padding=(K - u) // 2)
     yr.backward(_r16(dy))
-    _close(y, yr, "y")
-    _close(xd.grad, xr.grad, "dx")
+    _close(y, yr, "y", tol=TOL_Y)
+    _close(xd.grad, xr.grad, "dx", tol=TOL_Y)
     # d weight_v / weight_g go through the weight-norm reparametrisation on
     # both sides; compare the effective-weight gradient via the module's
     w_grad = torch.autograd.grad(
         torch._weight_norm(md.weight_v, md.weight_g, 0), [md.weight_v, md.weight_g],
         grad_outputs=wr.grad.to(device), allow_unused=True)
     _close(md.weight_v.grad, w_grad[0], "dweight_v")
-    _close(md.bias.grad, dy.sum((0, 2)), "db")
+    _close(md.bias.grad, (_r16(dy) if train_ops.TRAIN_IO16 else dy).sum((0, 2)), "db")
 
 
 @pytest.mark.parametrize("C,F,T,k0,s0", [(1, 65, 289, 5, 2), (1, 1025, 19, 5, 2),
@@ -262,13 +301,13 @@ def test_conv2d_freq_unfolded(device, C, F, T, k0, s0):
     ld = layer.to(device)
     xd = x.to(device).requires_grad_(True)
     y = D.conv2d_freq(ld, xd, train_ops.TRAIN_WDTYPE)
-    y.backward(dy.to(device))
+    y.backward(dy.to(device).to(y.dtype))
     wr = _r16(layer.weight.detach().cpu()).requires_grad_(True)
     br = layer.bias.detach().cpu().clone().requires_grad_(True)
     xr = _r16(x).requires_grad_(True)
     yr = F_.conv2d(xr, wr, br, stride=(s0, 1), padding=(0, 2))
     yr.backward(_r16(dy))
-    _close(y, yr, "y")
-    _close(xd.grad, xr.grad, "dx")
+    _close(y, yr, "y", tol=TOL_Y)
+    _close(xd.grad, xr.grad, "dx", tol=TOL_Y)
     _close(ld.weight.grad, wr.grad, "dw")
-    _close(ld.bias.grad, dy.sum((0, 2, 3)), "db")
+    _close(ld.bias.grad, (_r16(dy) if train_ops.TRAIN_IO16 else dy).sum((0, 2, 3)), "db")

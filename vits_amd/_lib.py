@@ -79,6 +79,8 @@ class ConvDesc(C.Structure):
         ("gmask_bstride", C.c_int64),
         ("gmask_cstride", C.c_int32),
         ("gmask_slope", C.c_float),
+        ("io16", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 
@@ -154,6 +156,8 @@ class ConvWgradDesc(C.Structure):
         ("dbias", C.c_void_p),
         ("wdtype", C.c_int32),
         ("reserved", C.c_int32),
+        ("io16", C.c_int32),
+        ("reserved2", C.c_int32),
     ]
 
 
@@ -259,6 +263,17 @@ _SIGS = {
         C.c_int, [C.POINTER(ResblockPairDesc), C.c_int, C.c_int, C.c_void_p]),
     "vits_resblock_pair_kc": (
         C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "vits_gate_forward_io16": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32,
+         C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p],
+    ),
+    "vits_gate_backward_io16": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64,
+         C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+         C.c_void_p],
+    ),
     "vits_radam_step": (
         C.c_int,
         [C.POINTER(RadamTensor), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,

@@ -44,6 +44,7 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
                  d.wdtype == VITS_WDT_F16);
   if (d.wdtype != VITS_WDT_F32) VITS_CHECK_SHAPE((d.kc % 16) == 0);
   if (d.gmask) VITS_CHECK_ARG(d.epi == VITS_EPI_STORE && d.split >= d.m);
+  if (d.io16) VITS_CHECK_ARG(d.wdtype != VITS_WDT_F32);
   return VITS_OK;
 }
 

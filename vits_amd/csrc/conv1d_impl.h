@@ -3,6 +3,8 @@
 // instantiation set each, compiled in parallel).  See conv1d.hip for the
 // design notes.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace vits_conv {
@@ -31,15 +33,29 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
+// element access of an I/O tensor of type OT (float, or the 16-bit operand
+// type for the IO16 kernels): OutDesc keeps float* fields, reinterpreted
+template <typename OT>
+__device__ __forceinline__ float ld_io(const float* base, int64_t i) {
+  return (float)reinterpret_cast<const OT*>(base)[i];
+}
+template <typename OT>
+__device__ __forceinline__ void st_io(float* base, int64_t i, float v) {
+  reinterpret_cast<OT*>(base)[i] = (OT)v;
+}
+
+template <typename OT>
 __device__ __forceinline__ void store_std(const OutDesc& o, int b, int ch, int t, float v,
                                           bool masked) {
   v = apply_act(v, o.act);
-  if (o.res) v = o.res[(int64_t)b * o.res_bstride + (int64_t)ch * o.res_cstride + t] + o.res_scale * v;
-  float* dst = o.y + (int64_t)b * o.y_bstride + (int64_t)ch * o.y_cstride + t;
-  if (o.accumulate) v = *dst + v;
+  if (o.res)
+    v = ld_io<OT>(o.res, (int64_t)b * o.res_bstride + (int64_t)ch * o.res_cstride + t) +
+        o.res_scale * v;
+  const int64_t di = (int64_t)b * o.y_bstride + (int64_t)ch * o.y_cstride + t;
+  if (o.accumulate) v = ld_io<OT>(o.y, di) + v;
   if (o.post_div != 1.0f) v = v / o.post_div;
   if (masked) v = 0.f;
-  *dst = v;
+  st_io<OT>(o.y, di, v);
 }
 
 // Register budget of the global->LDS prefetch (per thread): the host packs
@@ -91,8 +107,13 @@ struct ConvGroup {
   int batch;  // utterances per member
 };
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4>
+// IO16 (16-bit operand types only): x, residuals, gmask and the outputs are
+// tensors of the operand type (the fp16-autocast training step keeps its
+// activations in fp16, as the reference's autocast convs return them),
+// half the bytes of the fp32-I/O kernel; accumulation stays fp32.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false>
 __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) {
+  static_assert(!IO16 || WT != VITS_WDT_F32, "IO16 needs a 16-bit operand type");
   const int gi = (int)blockIdx.z / G.batch;
   const vits_conv1d_desc& p = G.d[gi];
   if ((int)blockIdx.x * BN >= p.n_out || (int)blockIdx.y * BM >= p.m) return;
@@ -100,6 +121,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   typedef typename LowP<WT>::T lp_t;
   typedef lp_t lpx8 __attribute__((ext_vector_type(8)));
   typedef lp_t lpx4 __attribute__((ext_vector_type(4)));
+  typedef typename std::conditional<IO16, lp_t, float>::type io_t;  // x / res / y element
   constexpr int WM = BM / WAVES_M;
   constexpr int WN = BN / WAVES_N;
   constexpr int TM = WM / 32;
@@ -150,7 +172,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const float* xb = p.x + (int64_t)b * p.x_bstride;
+  const io_t* xb = reinterpret_cast<const io_t*>(p.x) + (int64_t)b * p.x_bstride;
   const int64_t xts = p.x_tstride;
   const int xstart = n0 - p.pad_left - xsh;  // V4: a multiple of 4
   const float slope = p.in_slope;
@@ -159,8 +181,9 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   constexpr int NU = V4 ? MAXX / 4 : MAXX;  // staging units per thread (blocks or elements)
   constexpr int UW = V4 ? 4 : 1;            // elements per unit
   typedef float f32x4v __attribute__((ext_vector_type(4)));
-  f32x4v xreg4[V4 ? NU : 1];
-  float xreg[V4 ? 1 : NU];
+  typedef typename std::conditional<IO16, lpx4, f32x4v>::type x4_t;  // 16-byte / 8-byte unit
+  x4_t xreg4[V4 ? NU : 1];
+  io_t xreg[V4 ? 1 : NU];
   int xrow[NU];  // window row of unit tid + 256q (1<<24 when it is padding)
   int xoff[NU];  // its global offset relative to row 0 of the chunk
   const int nunits = V4 ? kc * nb : xsz;
@@ -203,15 +226,15 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   // compiler cannot tie a wait to each load: all MAXX loads stay in flight
   // under the chunk's MFMAs and are consumed in lstore.
   auto gload = [&](int c0) {
-    const float* base = xb + (int64_t)c0 * p.x_cstride;
+    const io_t* base = xb + (int64_t)c0 * p.x_cstride;
     const int lim = p.cin - c0;  // rows >= lim are channel padding
 #pragma unroll
     for (int q = 0; q < NU; ++q) {
       if (q * 256 < nunits) {  // workgroup-uniform: no exec-mask branch
         const bool ok = xrow[q] < lim;
-        const float* src = ok ? base + xoff[q] : xb;
+        const io_t* src = ok ? base + xoff[q] : xb;
         if constexpr (V4)
-          xreg4[q] = *reinterpret_cast<const f32x4v*>(src);
+          xreg4[q] = *reinterpret_cast<const x4_t*>(src);
         else
           xreg[q] = *src;
       }
@@ -228,10 +251,10 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
         const bool ok = xrow[q] < lim;
         if (u < nunits) {
           if constexpr (V4) {
-            f32x4v v = xreg4[q];
+            f32x4v v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float t = v[e];
+              float t = (float)xreg4[q][e];
               if (act_in) t = t < 0.f ? t * slope : t;
               v[e] = ok ? t : 0.f;
             }
@@ -245,7 +268,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
               *reinterpret_cast<f32x4v*>(xs + r * xrs + 4 * c) = v;
             }
           } else {
-            float v = xreg[q];
+            float v = (float)xreg[q];
             if (act_in) v = v < 0.f ? v * slope : v;
             v = ok ? v : 0.f;
             if constexpr (BF) {
@@ -440,7 +463,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
               const float va = acc[mi][ni][r] + erow[rloc + ro];
               const float vb = acc[mi][ni][r + 1] + erow[rloc + ro + 1];
               const float v = fast_tanh(va) * fast_sigmoid(vb);
-              store_std(o0, b, row >> 1, n, v, n >= len_b);
+              store_std<io_t>(o0, b, row >> 1, n, v, n >= len_b);
             }
           }
         }
@@ -456,7 +479,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
             const int t = n * u + ph - p.up_pad;
             if (t >= 0 && t < p.t_out) {
               const float v = acc[mi][ni][r] + erow[rloc + ro];
-              store_std(o0, b, oc, t, v, t >= len_b);
+              store_std<io_t>(o0, b, oc, t, v, t >= len_b);
             }
           }
         }
@@ -472,9 +495,9 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
             if (row < p.m) {
               const float v = acc[mi][ni][r] + erow[rloc + ro];
               if (row < p.split)
-                store_std(o0, b, row, n, v, n >= len_b);
+                store_std<io_t>(o0, b, row, n, v, n >= len_b);
               else
-                store_std(o1, b, row - p.split, n, v, n >= len_b);
+                store_std<io_t>(o1, b, row - p.split, n, v, n >= len_b);
             }
           }
         }
@@ -489,24 +512,24 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
           for (int r = 0; r < 16; ++r)
             v[r] = apply_act(acc[mi][ni][r] + erow[rloc + (r & 3) + 8 * (r >> 2)], o0.act);
           if (p.gmask) {  // leaky-relu derivative of the forward input
-            const float* gb = p.gmask + (int64_t)b * p.gmask_bstride + n;
+            const int64_t gb = (int64_t)b * p.gmask_bstride + n;
             float gv[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              gv[r] = gb[(int64_t)(row < p.m ? row : 0) * p.gmask_cstride];
+              gv[r] = ld_io<io_t>(p.gmask, gb + (int64_t)(row < p.m ? row : 0) * p.gmask_cstride);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = gv[r] > 0.f ? v[r] : v[r] * p.gmask_slope;
           }
-          float* yb = o0.y + (int64_t)b * o0.y_bstride + n;
+          const int64_t yb = (int64_t)b * o0.y_bstride + n;
           if (o0.res) {
-            const float* rb = o0.res + (int64_t)b * o0.res_bstride + n;
+            const int64_t rb = (int64_t)b * o0.res_bstride + n;
             float rv[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              rv[r] = rb[(int64_t)(row < p.m ? row : 0) * o0.res_cstride];
+              rv[r] = ld_io<io_t>(o0.res, rb + (int64_t)(row < p.m ? row : 0) * o0.res_cstride);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = rv[r] + o0.res_scale * v[r];
@@ -516,7 +539,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              yo[r] = yb[(int64_t)(row < p.m ? row : 0) * o0.y_cstride];
+              yo[r] = ld_io<io_t>(o0.y, yb + (int64_t)(row < p.m ? row : 0) * o0.y_cstride);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = yo[r] + v[r];
@@ -528,7 +551,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
             float t = v[r];
             if (o0.post_div != 1.0f) t = t / o0.post_div;
             if (msk) t = 0.f;
-            if (row < p.m) yb[(int64_t)row * o0.y_cstride] = t;
+            if (row < p.m) st_io<io_t>(o0.y, yb + (int64_t)row * o0.y_cstride, t);
           }
         }
       }
@@ -536,7 +559,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   }
 }
 
-template <int BM, int BN, int WM_, int WN_, int WT, bool V4>
+template <int BM, int BN, int WM_, int WN_, int WT, bool V4, bool IO16>
 int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
   constexpr bool BF = WT != VITS_WDT_F32;
   size_t lds = 0;
@@ -564,15 +587,15 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
   switch (d.epi) {
     case VITS_EPI_STORE:
       if (d.split < d.m)
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, WT, V4>), grid, block, lds, s, g);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, WT, V4, IO16>), grid, block, lds, s, g);
       else
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, WT, V4>), grid, block, lds, s, g);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, WT, V4, IO16>), grid, block, lds, s, g);
       break;
     case VITS_EPI_GATE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, WT, V4>), grid, block, lds, s, g);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, WT, V4, IO16>), grid, block, lds, s, g);
       break;
     case VITS_EPI_UPSAMPLE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, WT, V4>), grid, block, lds, s, g);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, WT, V4, IO16>), grid, block, lds, s, g);
       break;
     default:
       return VITS_E_UNSUP;
@@ -588,22 +611,33 @@ template <int BM, int BN, int WM_, int WN_, int WT>
 int launch_tile(const ConvGroup& g, hipStream_t s) {
   constexpr bool BF = WT != VITS_WDT_F32;
   size_t xrs4[VITS_CONV_GROUP], xrs1[VITS_CONV_GROUP];
-  int nv4 = 0;
+  int nv4 = 0, nio = 0;
   for (int i = 0; i < g.n; ++i) {
     const vits_conv1d_desc& d = g.d[i];
     const int xw = BN + (d.k - 1) * d.dil;
     xrs1[i] = (xw + 3) & ~3;
     const int xsh = (d.pad_left & 3) ? 4 - (d.pad_left & 3) : 0;
     xrs4[i] = 4 * ((xw + xsh + 3) >> 2);
+    // 16-byte (fp32) / 8-byte (IO16) blocks of 4 time steps
+    const int align = d.io16 ? 7 : 15;
     const bool v4 = d.x_tstride == 1 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
                     (d.tin & 3) == 0 && d.pad_left >= 0 &&
-                    (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(d.x) & align) == 0 &&
                     (size_t)d.kc * xrs4[i] <= (size_t)XTile<BN, BF>::floats;
     nv4 += v4;
+    nio += d.io16 != 0;
   }
-  if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true>(g, s, xrs4);
+  if (nio != 0 && (nio != g.n || !BF)) return VITS_E_UNSUP;
+  if constexpr (BF) {
+    if (nio) {
+      if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, true>(g, s, xrs4);
+      if (nv4 != 0) return VITS_E_UNSUP;
+      return launch_tile_v<BM, BN, WM_, WN_, WT, false, true>(g, s, xrs1);
+    }
+  }
+  if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, false>(g, s, xrs4);
   if (nv4 != 0) return VITS_E_UNSUP;
-  return launch_tile_v<BM, BN, WM_, WN_, WT, false>(g, s, xrs1);
+  return launch_tile_v<BM, BN, WM_, WN_, WT, false, false>(g, s, xrs1);
 }
 
 template <int WT>

@@ -80,7 +80,10 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 // consecutive steps of a channel pair from a 4-aligned window start (sh
 // rows of shift, read back with the same shift) - a quarter of the load
 // instructions of the element-wise map.
-template <int NK, int WT, bool PARTIAL, bool VEC>
+// IO16 (with VEC): dY and X are tensors of the 16-bit operand type (the
+// fp16 activations of the autocast training step); the 8-byte blocks stay
+// raw in registers until they are written to LDS.
+template <int NK, int WT, bool PARTIAL, bool VEC, bool IO16 = false>
 __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_conv1d_wgrad_desc p,
                                                                      int tchunks, int total_chunks,
                                                                      int chunks_per_wg,
@@ -127,7 +130,65 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
   // VEC window: rows from the 4-aligned start t0 - pad_left - sh
   const int sh = VEC ? ((p.pad_left & 3) ? 4 - (p.pad_left & 3) : 0) : 0;
 
+  typedef typename Op16<WT>::T T16;
+  typedef T16 t16x4 __attribute__((ext_vector_type(4)));
+  t16x4 dyr[IO16 ? 4 : 1], xr[IO16 ? 8 : 1];  // raw IO16 blocks
+  auto gload_io16 = [&](int chunk) {
+    const int b = chunk / tchunks;
+    const int t0 = (chunk - b * tchunks) * KT;
+    const T16* dyb = reinterpret_cast<const T16*>(p.dy) + (int64_t)b * p.dy_bstride;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const int co = m0 + (u >> 4);
+      const int t = t0 + 4 * (u & 15);
+      const T16* src = dyb + (int64_t)co * p.dy_cstride + t;
+      t16x4 v = {};
+      if (co < p.cout) {
+        if (t + 3 < p.n_out) {
+          v = *reinterpret_cast<const t16x4*>(src);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = t + e < p.n_out ? src[e] : (T16)0.f;
+        }
+      }
+      dyr[q] = v;
+    }
+    const T16* xb = reinterpret_cast<const T16*>(p.x) + (int64_t)b * p.x_bstride;
+    const int ts = t0 - p.pad_left - sh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const int ci = c0 + 2 * (u >> 5);
+      const int r4 = 4 * (u & 31);
+      const int t = ts + r4;
+      const bool tok = r4 < wr + sh && t >= 0 && t < p.tin;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        t16x4 v = {};
+        if (tok && ci + e < p.cin)
+          v = *reinterpret_cast<const t16x4*>(xb + (int64_t)(ci + e) * p.x_cstride + t);
+        xr[2 * q + e] = v;
+      }
+    }
+  };
+  auto unpack_io16 = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dyv[4 * q + e] = (float)dyr[q][e];
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xv[8 * q + 4 * e + i] = (float)xr[2 * q + e][i];
+    }
+  };
+
   auto gload_vec = [&](int chunk) {
+    if constexpr (IO16) {
+      gload_io16(chunk);
+      return;
+    }
     const int b = chunk / tchunks;
     const int t0 = (chunk - b * tchunks) * KT;
     const float* dyb = p.dy + (int64_t)b * p.dy_bstride;
@@ -169,6 +230,7 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
     }
   };
   auto lstore_vec = [&](uint16_t* st) {
+    if constexpr (IO16) unpack_io16();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int u = tid + 256 * q;
@@ -450,16 +512,21 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
   dim3 grid(w.splits, (d.cin + WG_N - 1) / WG_N, (d.cout + WG_M - 1) / WG_M);
   const size_t lds = 2 * STAGE_HALVES * sizeof(uint16_t);
   const int sh = (d.pad_left & 3) ? 4 - (d.pad_left & 3) : 0;
+  const uintptr_t al = d.io16 ? 7 : 15;
   const bool vec = (d.dy_cstride & 3) == 0 && (d.dy_bstride & 3) == 0 &&
-                   (reinterpret_cast<uintptr_t>(d.dy) & 15) == 0 && (d.x_cstride & 3) == 0 &&
-                   (d.x_bstride & 3) == 0 && (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(d.dy) & al) == 0 && (d.x_cstride & 3) == 0 &&
+                   (d.x_bstride & 3) == 0 && (reinterpret_cast<uintptr_t>(d.x) & al) == 0 &&
                    (d.tin & 3) == 0 && KT + (d.k - 1) * d.dil + sh <= MAX_WR &&
-                   d.k > 1;  // k = 1 (tools/wgrad_split_bench.py: 40 -> 53 us) keeps the
-                             // element-wise map: half the VEC units idle at a 64-row window
+                   (d.k > 1 || d.io16);  // k = 1 (tools/wgrad_split_bench.py: 40 -> 53 us)
+                                         // keeps the element-wise map for fp32 inputs
+  if (d.io16 && !vec) return VITS_E_UNSUP;  // IO16 needs aligned [B][C][T] operands
   switch (d.k) {
 #define VITS_WG_CASE(NK)                                                                           \
   case NK:                                                                                         \
-    if (vec)                                                                                       \
+    if (d.io16)                                                                                    \
+      hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL, true, true>), grid, dim3(256), lds, s, d,  \
+                         tchunks, total, cpw, ws, ws_b);                                           \
+    else if (vec)                                                                                  \
       hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL, true>), grid, dim3(256), lds, s, d,        \
                          tchunks, total, cpw, ws, ws_b);                                           \
     else                                                                                           \

@@ -7,61 +7,66 @@
 // output of a conv under autograd: ~5 elementwise kernels forward and ~8
 // backward in PyTorch, here one each.  The backward also reduces the cond
 // gradient dg[b][c] = sum_t dx[b][c][t] in the same pass (one workgroup per
-// (b, p) row pair, no atomics).  fp32 in / out; the rows are time-contiguous
-// with arbitrary batch / channel strides (channel slices of a larger
-// buffer are fine).
+// (b, p) row pair, no atomics).  fp32 in / out, or (the *_io16 entry
+// points) x / g / y / dy / dx of a 16-bit type with fp32 math and an fp32
+// dg; the rows are time-contiguous with arbitrary batch / channel strides
+// (channel slices of a larger buffer are fine).
 #include "common.h"
 
 namespace {
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-__global__ __launch_bounds__(256) void gate_fwd_kernel(const float* __restrict__ x, int64_t x_bs,
-                                                      int x_cs, const float* __restrict__ g,
-                                                      int64_t g_bs, float* __restrict__ y,
+template <typename E>
+__global__ __launch_bounds__(256) void gate_fwd_kernel(const E* __restrict__ x, int64_t x_bs,
+                                                      int x_cs, const E* __restrict__ g,
+                                                      int64_t g_bs, E* __restrict__ y,
                                                       int64_t y_bs, int y_cs, int H, int T) {
   const int p = blockIdx.x;
   const int b = blockIdx.y;
-  const float* xa = x + (int64_t)b * x_bs + (int64_t)p * x_cs;
-  const float* xb = xa + (int64_t)H * x_cs;
-  float* yr = y + (int64_t)b * y_bs + (int64_t)p * y_cs;
-  const float ga = g ? g[(int64_t)b * g_bs + p] : 0.f;
-  const float gb = g ? g[(int64_t)b * g_bs + H + p] : 0.f;
+  const E* xa = x + (int64_t)b * x_bs + (int64_t)p * x_cs;
+  const E* xb = xa + (int64_t)H * x_cs;
+  E* yr = y + (int64_t)b * y_bs + (int64_t)p * y_cs;
+  const float ga = g ? (float)g[(int64_t)b * g_bs + p] : 0.f;
+  const float gb = g ? (float)g[(int64_t)b * g_bs + H + p] : 0.f;
   for (int t = threadIdx.x; t < T; t += 256) {
-    const float a = tanhf(xa[t] + ga);
-    const float s = sigm(xb[t] + gb);
-    yr[t] = a * s;
+    const float a = tanhf((float)xa[t] + ga);
+    const float s = sigm((float)xb[t] + gb);
+    yr[t] = (E)(a * s);
   }
 }
 
-__global__ __launch_bounds__(256) void gate_bwd_kernel(const float* __restrict__ dy, int64_t dy_bs,
-                                                      int dy_cs, const float* __restrict__ x,
+template <typename E>
+__global__ __launch_bounds__(256) void gate_bwd_kernel(const E* __restrict__ dy, int64_t dy_bs,
+                                                      int dy_cs, const E* __restrict__ x,
                                                       int64_t x_bs, int x_cs,
-                                                      const float* __restrict__ g, int64_t g_bs,
-                                                      float* __restrict__ dx, int64_t dx_bs,
+                                                      const E* __restrict__ g, int64_t g_bs,
+                                                      E* __restrict__ dx, int64_t dx_bs,
                                                       int dx_cs, float* __restrict__ dg, int H,
                                                       int T) {
   __shared__ float red[2][4];
   const int p = blockIdx.x;
   const int b = blockIdx.y;
-  const float* xa = x + (int64_t)b * x_bs + (int64_t)p * x_cs;
-  const float* xb = xa + (int64_t)H * x_cs;
-  const float* dyr = dy + (int64_t)b * dy_bs + (int64_t)p * dy_cs;
-  float* dxa = dx + (int64_t)b * dx_bs + (int64_t)p * dx_cs;
-  float* dxb = dxa + (int64_t)H * dx_cs;
-  const float ga = g ? g[(int64_t)b * g_bs + p] : 0.f;
-  const float gb = g ? g[(int64_t)b * g_bs + H + p] : 0.f;
+  const E* xa = x + (int64_t)b * x_bs + (int64_t)p * x_cs;
+  const E* xb = xa + (int64_t)H * x_cs;
+  const E* dyr = dy + (int64_t)b * dy_bs + (int64_t)p * dy_cs;
+  E* dxa = dx + (int64_t)b * dx_bs + (int64_t)p * dx_cs;
+  E* dxb = dxa + (int64_t)H * dx_cs;
+  const float ga = g ? (float)g[(int64_t)b * g_bs + p] : 0.f;
+  const float gb = g ? (float)g[(int64_t)b * g_bs + H + p] : 0.f;
   float sa = 0.f, sb = 0.f;
   for (int t = threadIdx.x; t < T; t += 256) {
-    const float a = tanhf(xa[t] + ga);
-    const float s = sigm(xb[t] + gb);
-    const float d = dyr[t];
-    const float da = d * s * (1.0f - a * a);
-    const float db = d * a * s * (1.0f - s);
+    const float a = tanhf((float)xa[t] + ga);
+    const float s = sigm((float)xb[t] + gb);
+    const float d = (float)dyr[t];
+    // dg sums the gradients as stored (rounded to E, as the reference's
+    // autocast sum of the fp16 gradient would see them)
+    const E da = (E)(d * s * (1.0f - a * a));
+    const E db = (E)(d * a * s * (1.0f - s));
     dxa[t] = da;
     dxb[t] = db;
-    sa += da;
-    sb += db;
+    sa += (float)da;
+    sb += (float)db;
   }
   if (dg) {
     sa = wave_sum(sa);
@@ -87,7 +92,7 @@ extern "C" int vits_gate_forward(const float* x, int64_t x_bstride, int32_t x_cs
                                  void* stream) {
   VITS_CHECK_ARG(x && y && batch > 0 && half_channels > 0 && t_len > 0);
   VITS_CHECK_SHAPE(batch <= 65535);
-  hipLaunchKernelGGL(gate_fwd_kernel, dim3(half_channels, batch), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(gate_fwd_kernel<float>, dim3(half_channels, batch), dim3(256), 0, as_stream(stream),
                      x, x_bstride, x_cstride, g, g_bstride, y, y_bstride, y_cstride, half_channels,
                      t_len);
   return vits_launch_status();
@@ -100,8 +105,54 @@ extern "C" int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t d
                                   int t_len, void* stream) {
   VITS_CHECK_ARG(dy && x && dx && batch > 0 && half_channels > 0 && t_len > 0);
   VITS_CHECK_SHAPE(batch <= 65535);
-  hipLaunchKernelGGL(gate_bwd_kernel, dim3(half_channels, batch), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(gate_bwd_kernel<float>, dim3(half_channels, batch), dim3(256), 0, as_stream(stream),
                      dy, dy_bstride, dy_cstride, x, x_bstride, x_cstride, g, g_bstride, dx,
                      dx_bstride, dx_cstride, dg, half_channels, t_len);
+  return vits_launch_status();
+}
+
+extern "C" int vits_gate_forward_io16(const void* x, int64_t x_bstride, int32_t x_cstride,
+                                      const void* g, int64_t g_bstride, void* y,
+                                      int64_t y_bstride, int32_t y_cstride, int batch,
+                                      int half_channels, int t_len, int wdtype, void* stream) {
+  VITS_CHECK_ARG(x && y && batch > 0 && half_channels > 0 && t_len > 0);
+  VITS_CHECK_SHAPE(batch <= 65535);
+  const dim3 grid(half_channels, batch);
+  hipStream_t s = as_stream(stream);
+#define VITS_GATE_FWD(E)                                                                           \
+  hipLaunchKernelGGL(gate_fwd_kernel<E>, grid, dim3(256), 0, s, static_cast<const E*>(x),         \
+                     x_bstride, x_cstride, static_cast<const E*>(g), g_bstride, static_cast<E*>(y), \
+                     y_bstride, y_cstride, half_channels, t_len)
+  if (wdtype == VITS_WDT_F16)
+    VITS_GATE_FWD(_Float16);
+  else if (wdtype == VITS_WDT_BF16)
+    VITS_GATE_FWD(__bf16);
+  else
+    return VITS_E_ARG;
+#undef VITS_GATE_FWD
+  return vits_launch_status();
+}
+
+extern "C" int vits_gate_backward_io16(const void* dy, int64_t dy_bstride, int32_t dy_cstride,
+                                       const void* x, int64_t x_bstride, int32_t x_cstride,
+                                       const void* g, int64_t g_bstride, void* dx,
+                                       int64_t dx_bstride, int32_t dx_cstride, float* dg, int batch,
+                                       int half_channels, int t_len, int wdtype, void* stream) {
+  VITS_CHECK_ARG(dy && x && dx && batch > 0 && half_channels > 0 && t_len > 0);
+  VITS_CHECK_SHAPE(batch <= 65535);
+  const dim3 grid(half_channels, batch);
+  hipStream_t s = as_stream(stream);
+#define VITS_GATE_BWD(E)                                                                           \
+  hipLaunchKernelGGL(gate_bwd_kernel<E>, grid, dim3(256), 0, s, static_cast<const E*>(dy),        \
+                     dy_bstride, dy_cstride, static_cast<const E*>(x), x_bstride, x_cstride,      \
+                     static_cast<const E*>(g), g_bstride, static_cast<E*>(dx), dx_bstride,       \
+                     dx_cstride, dg, half_channels, t_len)
+  if (wdtype == VITS_WDT_F16)
+    VITS_GATE_BWD(_Float16);
+  else if (wdtype == VITS_WDT_BF16)
+    VITS_GATE_BWD(__bf16);
+  else
+    return VITS_E_ARG;
+#undef VITS_GATE_BWD
   return vits_launch_status();
 }

@@ -160,7 +160,7 @@ def conv2d_freq(layer, h, wdt):
     u = h.unfold(2, k0, s0)                                    # [B, C, F_out, T, k0]
     u = u.permute(0, 2, 1, 4, 3).reshape(B * F_out, C * k0, T)
     w = layer.weight.reshape(O, C * k0, k1)
-    y = train_ops.Conv1dHip.apply(u, w, layer.bias, 1, layer.padding[1], 1.0, wdt)
+    y = train_ops.conv1d_hip(u, w, layer.bias, 1, layer.padding[1], 1.0, wdt)
     return y.view(B, F_out, O, y.shape[2]).permute(0, 2, 1, 3)
 
 
@@ -338,7 +338,7 @@ class DiscriminatorP(nn.Module):
             w = _wn_weight(layer).squeeze(-1)
             s, pd = layer.stride[0], layer.padding[0]
             if s == 1 and _hip_wdtype(x) is not None:
-                x = train_ops.Conv1dHip.apply(x, w, layer.bias, 1, pd, 1.0, _hip_wdtype(x))
+                x = train_ops.conv1d_hip(x, w, layer.bias, 1, pd, 1.0, _hip_wdtype(x))
             elif MPD_GEMM and x.device.type == "cuda":
                 x = conv1d_gemm(x, w, layer.bias, s, pd)
             else:
@@ -347,7 +347,7 @@ class DiscriminatorP(nn.Module):
             fmap.append(x.view(b, p, x.shape[1], x.shape[2]).permute(0, 2, 3, 1))
         w = _wn_weight(self.conv_post).squeeze(-1)
         if _hip_wdtype(x) is not None:
-            x = train_ops.Conv1dHip.apply(x, w, self.conv_post.bias, 1, 1, 1.0, _hip_wdtype(x))
+            x = train_ops.conv1d_hip(x, w, self.conv_post.bias, 1, 1, 1.0, _hip_wdtype(x))
         else:
             x = F.conv1d(x, w, self.conv_post.bias, padding=1)
         x = x.view(b, p, 1, x.shape[2]).permute(0, 2, 3, 1)

@@ -265,12 +265,12 @@ def make_out(y: torch.Tensor, *, act: int = ACT_NONE, res: Optional[torch.Tensor
              res_scale: float = 1.0, accumulate: bool = False, post_div: float = 1.0,
              channel_offset: int = 0) -> ConvOut:
     o = ConvOut()
-    o.y = y.data_ptr() + 4 * channel_offset * y.stride(1)
+    o.y = y.data_ptr() + y.element_size() * channel_offset * y.stride(1)
     o.y_bstride = y.stride(0)
     o.y_cstride = y.stride(1)
     o.act = act
     if res is not None:
-        o.res = res.data_ptr() + 4 * channel_offset * res.stride(1)
+        o.res = res.data_ptr() + res.element_size() * channel_offset * res.stride(1)
         o.res_bstride = res.stride(0)
         o.res_cstride = res.stride(1)
     else:
@@ -283,14 +283,23 @@ def make_out(y: torch.Tensor, *, act: int = ACT_NONE, res: Optional[torch.Tensor
     return o
 
 
+_LOWP_TORCH = {WDT_F16: torch.float16, WDT_BF16: torch.bfloat16}
+
+
 def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Optional[ConvOut] = None,
               split: Optional[int] = None, tin: Optional[int] = None, n_out: Optional[int] = None,
               in_slope: float = 1.0, cond: Optional[torch.Tensor] = None, cond_offset: int = 0,
               lengths: Optional[torch.Tensor] = None, t_out: int = 0,
-              x_channel_offset: int = 0) -> ConvDesc:
-    assert x.dtype == torch.float32
+              x_channel_offset: int = 0, io16: bool = False) -> ConvDesc:
+    """io16: x / outputs / residuals / gmask are tensors of the layer's
+    16-bit operand type (the fp16 training convs); fp32 otherwise."""
+    if io16:
+        assert layer.wdtype != WDT_F32 and x.dtype == _LOWP_TORCH[layer.wdtype]
+    else:
+        assert x.dtype == torch.float32
     d = ConvDesc()
-    d.x = x.data_ptr() + 4 * x_channel_offset * x.stride(1)
+    d.x = x.data_ptr() + x.element_size() * x_channel_offset * x.stride(1)
+    d.io16 = int(io16)
     d.x_bstride = x.stride(0)
     d.x_cstride = x.stride(1)
     d.x_tstride = x.stride(2)

@@ -32,6 +32,8 @@ torch conv, i.e. the reference's own fp32 arithmetic.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -98,10 +100,13 @@ def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
 
 
 def _run(x: torch.Tensor, layer: PackedConv, n_out: int, in_slope: float = 1.0,
-         gmask: torch.Tensor | None = None, gmask_slope: float = 1.0) -> torch.Tensor:
+         gmask: torch.Tensor | None = None, gmask_slope: float = 1.0,
+         io16: bool = False) -> torch.Tensor:
     B = x.shape[0]
-    y = torch.empty(B, layer.m, n_out, device=x.device, dtype=torch.float32)
-    d = make_desc(layer, x, make_out(y), in_slope=in_slope, tin=x.shape[2], n_out=n_out)
+    y = torch.empty(B, layer.m, n_out, device=x.device,
+                    dtype=_TORCH_16[layer.wdtype] if io16 else torch.float32)
+    d = make_desc(layer, x, make_out(y), in_slope=in_slope, tin=x.shape[2], n_out=n_out,
+                  io16=io16)
     if gmask is not None:
         # leaky-relu derivative of the forward input, fused into the epilogue
         d.gmask, d.gmask_bstride, d.gmask_cstride = gmask.data_ptr(), gmask.stride(0), gmask.stride(1)
@@ -129,21 +134,34 @@ def use_split_wgrad(cout: int, cin: int, k: int) -> bool:
 SPLIT_WGRAD_MAX = 1 << 40
 
 
+def _wgrad_io16_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """The 16-bit-input weight gradient needs 8-byte aligned time rows."""
+    return (dy.dtype == x.dtype and dy.dtype in (torch.float16, torch.bfloat16)
+            and x.shape[2] % 4 == 0 and all(t.stride(0) % 4 == 0 and t.stride(1) % 4 == 0
+                                            and t.data_ptr() % 8 == 0 for t in (dy, x)))
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, k: int, dil: int, pad_left: int,
           in_slope: float = 1.0, with_bias: bool = True, wdtype: int = TRAIN_WDTYPE,
           buf: torch.Tensor | None = None, split: bool | None = None):
     """dW [Cout, Cin, k] and dbias [Cout] (fp32) of y = conv1d(act(x), W) + b.
     ``buf``: a zeroed wgrad_buffer (atomic mode; else one is allocated).
-    ``split``: split-K mode (default: ``use_split_wgrad``)."""
+    ``split``: split-K mode (default: ``use_split_wgrad``).  dy / x: fp32, or
+    both of the 16-bit operand type (read as such when aligned, else cast)."""
+    io16 = dy.dtype != torch.float32
+    if io16 and not _wgrad_io16_ok(dy, x):
+        dy, x, io16 = dy.float().contiguous(), x.float().contiguous(), False
     B, cout, n_out = dy.shape
     _, cin, tin = x.shape
-    assert dy.stride(2) == 1 and x.stride(2) == 1 and dy.dtype == x.dtype == torch.float32
+    assert dy.stride(2) == 1 and x.stride(2) == 1 and dy.dtype == x.dtype
+    assert io16 or dy.dtype == torch.float32
     if split is None:
         split = buf is None and use_split_wgrad(cout, cin, k)
     if split:
         dw = torch.empty(cout, cin, k, device=dy.device, dtype=torch.float32)
         db = torch.empty(cout, device=dy.device, dtype=torch.float32) if with_bias else None
         d = _wgrad_desc(dy, x, k, dil, pad_left, in_slope, dw, db, wdtype)
+        d.io16 = int(io16)
         lib = _lib.load()
         nws = int(lib.vits_conv1d_wgrad_workspace(d, B))
         ws = torch.empty(max(nws, 1), device=dy.device, dtype=torch.float32)
@@ -155,6 +173,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, k: int, dil: int, pad_left: int,
     dw_t = buf[:k * cout * cin].view(k, cout, cin)
     db = buf[k * cout * cin:] if with_bias else None
     d = _wgrad_desc(dy, x, k, dil, pad_left, in_slope, dw_t, db, wdtype)
+    d.io16 = int(io16)
     check(_lib.load().vits_conv1d_wgrad(d, B, _stream_ptr(dy.device)), "vits_conv1d_wgrad")
     if k == 1:  # [1][cout][cin] is already the parameter layout
         return dw_t.view(cout, cin, 1), db
@@ -268,10 +287,122 @@ class GateHip(torch.autograd.Function):
         return dx, dg
 
 
+class Conv1dHip16(torch.autograd.Function):
+    """Conv1dHip with 16-bit activations: x, y, dY and dX are tensors of the
+    operand type (fp16 under the reference's fp16 autocast, whose convs
+    return fp16), read and written as such by the kernels (io16); W and b
+    stay fp32 masters (packed to 16 bits per call), dW / db fp32."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, dilation: int, padding: int, in_slope: float, wdtype: int):
+        if x.stride(2) != 1:
+            x = x.contiguous()
+        w32 = weight.detach().float().contiguous()
+        k = w32.shape[2]
+        n_out = x.shape[2] + 2 * padding - (k - 1) * dilation
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        if ctx.needs_input_grad[0]:
+            layer, layer_t = _pack16_pair(w32, dilation, padding, wdtype, b32, n_out, x.shape[2])
+            ctx.layer_t = layer_t
+        else:
+            layer = _pack16(w32, False, dilation, padding, wdtype, b32, n_out=n_out)
+            ctx.layer_t = None
+        y = _run(x, layer, n_out, in_slope, io16=True)
+        ctx.save_for_backward(x, w32)
+        ctx.conf = (dilation, padding, in_slope, wdtype, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w32 = ctx.saved_tensors
+        dil, pad, slope, wdtype, has_bias = ctx.conf
+        k = w32.shape[2]
+        dy = dy.to(x.dtype)
+        if dy.stride(2) != 1:
+            dy = dy.contiguous()
+        dx = dw = db = None
+        want_w = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
+        if ctx.needs_input_grad[0]:
+            layer_t = ctx.layer_t
+            if layer_t is None:
+                layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, n_out=x.shape[2])
+            ctx.layer_t = None
+            dx = _run(dy, layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
+                      gmask_slope=slope, io16=True)
+        if want_w:
+            dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype,
+                           split=True)
+        return dx, dw, db, None, None, None, None
+
+
+class GateHip16(torch.autograd.Function):
+    """GateHip on 16-bit activations (x, g, y, dY, dX of the operand type;
+    the cond gradient is summed in fp32 and returned in g's type)."""
+
+    @staticmethod
+    def forward(ctx, x, g, wdtype: int):
+        B, C2, T = x.shape
+        H = C2 // 2
+        if x.stride(2) != 1:
+            x = x.contiguous()
+        if g is not None and g.stride(1) != 1:
+            g = g.contiguous()
+        y = torch.empty(B, H, T, device=x.device, dtype=x.dtype)
+        check(_lib.load().vits_gate_forward_io16(
+            x.data_ptr(), x.stride(0), x.stride(1), None if g is None else g.data_ptr(),
+            0 if g is None else g.stride(0), y.data_ptr(), y.stride(0), y.stride(1), B, H, T,
+            wdtype, _stream_ptr(x.device)), "vits_gate_forward_io16")
+        ctx.save_for_backward(x, g)
+        ctx.wdtype = wdtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, g = ctx.saved_tensors
+        B, C2, T = x.shape
+        H = C2 // 2
+        dy = dy.to(x.dtype)
+        if dy.stride(2) != 1:
+            dy = dy.contiguous()
+        dx = torch.empty(B, C2, T, device=x.device, dtype=x.dtype)
+        want_dg = g is not None and ctx.needs_input_grad[1]
+        dg = torch.empty(B, C2, device=x.device, dtype=torch.float32) if want_dg else None
+        check(_lib.load().vits_gate_backward_io16(
+            dy.data_ptr(), dy.stride(0), dy.stride(1), x.data_ptr(), x.stride(0), x.stride(1),
+            None if g is None else g.data_ptr(), 0 if g is None else g.stride(0), dx.data_ptr(),
+            dx.stride(0), dx.stride(1), None if dg is None else dg.data_ptr(), B, H, T,
+            ctx.wdtype, _stream_ptr(x.device)), "vits_gate_backward_io16")
+        return dx, (None if dg is None else dg.to(g.dtype)), None
+
+
+# 16-bit activations for the training convs / gates under fp16 autocast (the
+# reference's autocast convs return fp16); False: the fp32-I/O kernels
+TRAIN_IO16 = os.environ.get("VITS_TRAIN_IO16", "1") != "0"
+
+
+def _io16(wdt) -> bool:
+    return TRAIN_IO16 and wdt == WDT_F16
+
+
+def conv1d_hip(x: torch.Tensor, w: torch.Tensor, bias, dilation: int, padding: int,
+               in_slope: float, wdt: int) -> torch.Tensor:
+    """The HIP training conv of operand type ``wdt``: 16-bit activations
+    (Conv1dHip16; x cast to fp16 first, as autocast casts a conv's input) or
+    fp32 activations (Conv1dHip)."""
+    if _io16(wdt):
+        x16 = x if x.dtype == _TORCH_16[wdt] else x.to(_TORCH_16[wdt])
+        return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt)
+    return Conv1dHip.apply(x, w, bias, dilation, padding, in_slope, wdt)
+
+
 def gate(x: torch.Tensor, g) -> torch.Tensor:
     """The WN / ResBlock2 gate: the HIP op inside a 16-bit autocast region on
     a ROCm device (where the convs around it are HIP too), torch otherwise."""
-    if x.device.type == "cuda" and autocast_wdtype() is not None:
+    wdt = autocast_wdtype() if x.device.type == "cuda" else None
+    if wdt is not None and _io16(wdt) and x.dtype == _TORCH_16[wdt]:
+        g16 = None if g is None else g.to(x.dtype)
+        return GateHip16.apply(x, g16, wdt)
+    if x.device.type == "cuda" and wdt is not None:
         return GateHip.apply(x, g)
     H = x.shape[1] // 2
     if g is not None:
@@ -314,8 +445,7 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) -> torch.T
             x = F.leaky_relu(x, in_slope)
         return module(x)
     w = weight_norm_effective(module)
-    return Conv1dHip.apply(x, w, module.bias, module.dilation[0], module.padding[0], in_slope,
-                           wdt)
+    return conv1d_hip(x, w, module.bias, module.dilation[0], module.padding[0], in_slope, wdt)
 
 
 # ---------------------------------------------------------------------------
@@ -387,6 +517,6 @@ def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) 
     wp = wp.permute(0, 2, 1, 3).reshape(O * u, C, P + 1)
     bias = None if module.bias is None else module.bias.repeat_interleave(u)
     B, _, T = x.shape
-    y = Conv1dHip.apply(x, wp, bias, 1, P - 1 - c0, in_slope, wdt)  # [B, O*u, >= T]
+    y = conv1d_hip(x, wp, bias, 1, P - 1 - c0, in_slope, wdt)  # [B, O*u, >= T]
     # phases -> time: y[b][o*u + r][q] -> out[b][o][q*u + r]  (T_out = T*u)
     return y[:, :, :T].reshape(B, O, u, T).permute(0, 1, 3, 2).reshape(B, O, T * u)
