@@ -338,8 +338,7 @@ typedef struct vits_conv1d_wgrad_desc {
   int32_t reserved;       /* > 0: (b, t)-chunks of 64 steps per workgroup    */
                           /* (tuning override), 0 = automatic                */
   int32_t io16;           /* dy / x are tensors of the 16-bit operand type   */
-                          /* (strides in elements; 8-byte aligned rows,      */
-                          /* tin % 4 == 0, else VITS_E_UNSUP)                */
+                          /* (strides in elements)                           */
   int32_t reserved2;
 } vits_conv1d_wgrad_desc;
 /* dW[co][ci][j] = sum_{b,t} dY[b][co][t] * act(x[b][ci][t - pad_left + j*dil]) */

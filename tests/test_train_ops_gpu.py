@@ -220,15 +220,21 @@ def test_gate_fwd_bwd_io16(device, B, H, T, with_g):
     (5, 1024, 1, 3, 1, 1, 11, 1.0),        # MPD conv_post: one output row, T < 64
     (4, 64, 64, 5, 9, 0, 4097, 0.2),       # many (b, t) chunks, odd length
 ])
-def test_wgrad_atomic_and_split_modes(device, B, cin, cout, k, dil, pad, T, slope, split):
+@pytest.mark.parametrize("io16", [False, True])
+def test_wgrad_atomic_and_split_modes(device, B, cin, cout, k, dil, pad, T, slope, split, io16):
     """Both weight-gradient modes (fp32 atomics into [k][cout][cin]; split-K
     partial tiles + reduce written in [cout][cin][k]) against torch fp32 on
-    the same fp16-rounded operands."""
+    the same fp16-rounded operands; fp32 or fp16 (io16) dY / x tensors
+    (aligned rows: 8-byte block loads; odd lengths: element loads)."""
     g = torch.Generator().manual_seed(cin * 17 + cout + k + T)
     x = torch.randn(B, cin, T, generator=g)
     T_out = T + 2 * pad - (k - 1) * dil
     dy = torch.randn(B, cout, T_out, generator=g)
-    dw, db = train_ops.wgrad(dy.to(device), x.to(device), k, dil, pad, slope, split=split)
+    if io16:
+        x, dy = _r16(x), _r16(dy)
+    cast = (lambda t: t.half()) if io16 else (lambda t: t)
+    dw, db = train_ops.wgrad(cast(dy).to(device), cast(x).to(device), k, dil, pad, slope,
+                             split=split)
     xr = _r16(F.leaky_relu(x, slope) if slope != 1.0 else x)
     wr = torch.zeros(cout, cin, k, requires_grad=True)
     F.conv1d(xr, wr, None, padding=pad, dilation=dil).backward(_r16(dy))
@@ -311,3 +317,32 @@ def test_conv2d_freq_unfolded(device, C, F, T, k0, s0):
     _close(xd.grad, xr.grad, "dx", tol=TOL_Y)
     _close(ld.weight.grad, wr.grad, "dw")
     _close(ld.bias.grad, (_r16(dy) if train_ops.TRAIN_IO16 else dy).sum((0, 2, 3)), "db")
+
+
+def test_conv1d_train_io16_residual(device):
+    """Conv1dHip16 with the residual in the epilogue (ResBlock2's
+    ``x = c2(xt) + x``): y = res + conv, d res = dY, and the other gradients
+    as without the residual."""
+    g = torch.Generator().manual_seed(5)
+    B, cin, cout, k, T = 2, 16, 32, 7, 600
+    x = _r16(torch.randn(B, cin, T, generator=g))
+    w = torch.randn(cout, cin, k, generator=g) / (cin * k) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    r = _r16(torch.randn(B, cout, T, generator=g))
+    dy = _r16(torch.randn(B, cout, T, generator=g))
+    xd = x.half().to(device).requires_grad_(True)
+    wd = w.to(device).requires_grad_(True)
+    bd = b.to(device).requires_grad_(True)
+    rd = r.half().to(device).requires_grad_(True)
+    y = train_ops.Conv1dHip16.apply(xd, wd, bd, 1, 3, 1.0, train_ops.TRAIN_WDTYPE, rd)
+    y.backward(dy.half().to(device))
+    xr = x.clone().requires_grad_(True)
+    wr = _r16(w).requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    rr = r.clone().requires_grad_(True)
+    yr = F.conv1d(xr, wr, br, padding=3) + rr
+    yr.backward(dy)
+    _close(y, yr, "y", tol=TOL16)
+    _close(rd.grad, rr.grad, "dres", tol=0)
+    _close(xd.grad, xr.grad, "dx", tol=TOL16)
+    _close(wd.grad, wr.grad, "dw")

@@ -31,6 +31,8 @@
 // combine them stay far below the chip's atomic byte rate); partial tiles
 // are added with global_atomic_add_f32 into a [k][Cout][Cin] accumulator
 // (two 128-byte row segments per wave instruction).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -260,20 +262,24 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
     }
   };
 
+  // element-wise map; with IO16 the 16-bit values stay raw in registers
+  // (dyh / xh) until lstore converts them
+  typedef typename std::conditional<IO16, T16, float>::type el_t;
+  el_t dyh[16], xh[32];
   auto gload = [&](int chunk) {
     const int b = chunk / tchunks;
     const int t0 = (chunk - b * tchunks) * KT;
-    const float* dyb = p.dy + (int64_t)b * p.dy_bstride;
+    const el_t* dyb = reinterpret_cast<const el_t*>(p.dy) + (int64_t)b * p.dy_bstride;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int co = m0 + dy_row0 + 8 * q;
       const int t = t0 + dy_col;
-      const float* src = dyb + (int64_t)co * p.dy_cstride + t;
+      const el_t* src = dyb + (int64_t)co * p.dy_cstride + t;
       const bool rok = co < p.cout;
-      dyv[2 * q] = (rok && t < p.n_out) ? src[0] : 0.f;
-      dyv[2 * q + 1] = (rok && t + 1 < p.n_out) ? src[1] : 0.f;
+      dyh[2 * q] = (rok && t < p.n_out) ? src[0] : (el_t)0.f;
+      dyh[2 * q + 1] = (rok && t + 1 < p.n_out) ? src[1] : (el_t)0.f;
     }
-    const float* xb = p.x + (int64_t)b * p.x_bstride;
+    const el_t* xb = reinterpret_cast<const el_t*>(p.x) + (int64_t)b * p.x_bstride;
     const int ts = t0 - p.pad_left;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -286,12 +292,16 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const bool ok = tok && ci + e < p.cin;
-          xv[(i * 2 + h) * 2 + e] = ok ? xb[(int64_t)(ci + e) * p.x_cstride + t] : 0.f;
+          xh[(i * 2 + h) * 2 + e] = ok ? xb[(int64_t)(ci + e) * p.x_cstride + t] : (el_t)0.f;
         }
       }
     }
   };
   auto lstore = [&](uint16_t* st) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dyv[i] = (float)dyh[i];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) xv[i] = (float)xh[i];
     uint32_t* dyl = reinterpret_cast<uint32_t*>(st);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -519,12 +529,14 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
                    (d.tin & 3) == 0 && KT + (d.k - 1) * d.dil + sh <= MAX_WR &&
                    (d.k > 1 || d.io16);  // k = 1 (tools/wgrad_split_bench.py: 40 -> 53 us)
                                          // keeps the element-wise map for fp32 inputs
-  if (d.io16 && !vec) return VITS_E_UNSUP;  // IO16 needs aligned [B][C][T] operands
   switch (d.k) {
 #define VITS_WG_CASE(NK)                                                                           \
   case NK:                                                                                         \
-    if (d.io16)                                                                                    \
+    if (d.io16 && vec)                                                                             \
       hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL, true, true>), grid, dim3(256), lds, s, d,  \
+                         tchunks, total, cpw, ws, ws_b);                                           \
+    else if (d.io16)                                                                               \
+      hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL, false, true>), grid, dim3(256), lds, s, d, \
                          tchunks, total, cpw, ws, ws_b);                                           \
     else if (vec)                                                                                  \
       hipLaunchKernelGGL((wgrad_kernel<NK, WT, PARTIAL, true>), grid, dim3(256), lds, s, d,        \

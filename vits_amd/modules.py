@@ -118,7 +118,9 @@ class ResBlock2(nn.Module):
         for c1, c2, cs in zip(self.convs1, self.convs2, self.conds):
             xt = train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE)
             xt = train_ops.gate(xt, cs(g))
-            x = train_ops.conv1d(c2, xt) + x
+            # modules.py:258-259 (xt = c2(xt); x = xt + x): the add in the
+            # conv epilogue on the fp16 training path
+            x = train_ops.conv1d(c2, xt, residual=x)
         return x
 
     def infer(self, x, g=None):

@@ -101,11 +101,11 @@ def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
 
 def _run(x: torch.Tensor, layer: PackedConv, n_out: int, in_slope: float = 1.0,
          gmask: torch.Tensor | None = None, gmask_slope: float = 1.0,
-         io16: bool = False) -> torch.Tensor:
+         io16: bool = False, res: torch.Tensor | None = None) -> torch.Tensor:
     B = x.shape[0]
     y = torch.empty(B, layer.m, n_out, device=x.device,
                     dtype=_TORCH_16[layer.wdtype] if io16 else torch.float32)
-    d = make_desc(layer, x, make_out(y), in_slope=in_slope, tin=x.shape[2], n_out=n_out,
+    d = make_desc(layer, x, make_out(y, res=res), in_slope=in_slope, tin=x.shape[2], n_out=n_out,
                   io16=io16)
     if gmask is not None:
         # leaky-relu derivative of the forward input, fused into the epilogue
@@ -135,10 +135,9 @@ SPLIT_WGRAD_MAX = 1 << 40
 
 
 def _wgrad_io16_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
-    """The 16-bit-input weight gradient needs 8-byte aligned time rows."""
-    return (dy.dtype == x.dtype and dy.dtype in (torch.float16, torch.bfloat16)
-            and x.shape[2] % 4 == 0 and all(t.stride(0) % 4 == 0 and t.stride(1) % 4 == 0
-                                            and t.data_ptr() % 8 == 0 for t in (dy, x)))
+    """dy and x of one 16-bit type: read as such by the weight-gradient
+    kernel (8-byte block loads when aligned, element loads otherwise)."""
+    return dy.dtype == x.dtype and dy.dtype in (torch.float16, torch.bfloat16)
 
 
 def wgrad(dy: torch.Tensor, x: torch.Tensor, k: int, dil: int, pad_left: int,
@@ -294,7 +293,10 @@ class Conv1dHip16(torch.autograd.Function):
     stay fp32 masters (packed to 16 bits per call), dW / db fp32."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, dilation: int, padding: int, in_slope: float, wdtype: int):
+    def forward(ctx, x, weight, bias, dilation: int, padding: int, in_slope: float, wdtype: int,
+                res=None):
+        """res (optional, fp16 [B, Cout, n_out]): y = res + conv, the
+        residual add of ResBlock2 (modules.py:258-259) in the epilogue."""
         if x.stride(2) != 1:
             x = x.contiguous()
         w32 = weight.detach().float().contiguous()
@@ -307,7 +309,11 @@ class Conv1dHip16(torch.autograd.Function):
         else:
             layer = _pack16(w32, False, dilation, padding, wdtype, b32, n_out=n_out)
             ctx.layer_t = None
-        y = _run(x, layer, n_out, in_slope, io16=True)
+        if res is not None:
+            assert res.dtype == x.dtype and res.shape == (x.shape[0], layer.m, n_out)
+            if res.stride(2) != 1:
+                res = res.contiguous()
+        y = _run(x, layer, n_out, in_slope, io16=True, res=res)
         ctx.save_for_backward(x, w32)
         ctx.conf = (dilation, padding, in_slope, wdtype, bias is not None)
         return y
@@ -332,7 +338,10 @@ class Conv1dHip16(torch.autograd.Function):
         if want_w:
             dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype,
                            split=True)
-        return dx, dw, db, None, None, None, None
+        if len(ctx.needs_input_grad) == 7:  # called without the residual argument
+            return dx, dw, db, None, None, None, None
+        dres = dy if ctx.needs_input_grad[7] else None
+        return dx, dw, db, None, None, None, None, dres
 
 
 class GateHip16(torch.autograd.Function):
@@ -385,14 +394,21 @@ def _io16(wdt) -> bool:
 
 
 def conv1d_hip(x: torch.Tensor, w: torch.Tensor, bias, dilation: int, padding: int,
-               in_slope: float, wdt: int) -> torch.Tensor:
-    """The HIP training conv of operand type ``wdt``: 16-bit activations
-    (Conv1dHip16; x cast to fp16 first, as autocast casts a conv's input) or
-    fp32 activations (Conv1dHip)."""
+               in_slope: float, wdt: int, residual: torch.Tensor | None = None) -> torch.Tensor:
+    """The HIP training conv of operand type ``wdt`` (+ ``residual``): 16-bit
+    activations (Conv1dHip16; x cast to fp16 first, as autocast casts a
+    conv's input; the residual added in the epilogue) or fp32 activations
+    (Conv1dHip)."""
     if _io16(wdt):
-        x16 = x if x.dtype == _TORCH_16[wdt] else x.to(_TORCH_16[wdt])
-        return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt)
-    return Conv1dHip.apply(x, w, bias, dilation, padding, in_slope, wdt)
+        t16 = _TORCH_16[wdt]
+        x16 = x if x.dtype == t16 else x.to(t16)
+        if residual is not None and residual.dtype != t16:
+            # an fp32 residual stream keeps the reference's fp32 add
+            return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt,
+                                     None) + residual
+        return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt, residual)
+    y = Conv1dHip.apply(x, w, bias, dilation, padding, in_slope, wdt)
+    return y if residual is None else y + residual
 
 
 def gate(x: torch.Tensor, g) -> torch.Tensor:
@@ -429,9 +445,10 @@ def autocast_wdtype(device_type: str = "cuda"):
     return {torch.float16: WDT_F16, torch.bfloat16: WDT_BF16}.get(dt)
 
 
-def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) -> torch.Tensor:
-    """``module(leaky_relu(x, in_slope))`` for an nn.Conv1d (optionally
-    legacy-weight-normed or spectral-normed).
+def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0,
+           residual: torch.Tensor | None = None) -> torch.Tensor:
+    """``module(leaky_relu(x, in_slope)) (+ residual)`` for an nn.Conv1d
+    (optionally legacy-weight-normed or spectral-normed).
 
     Inside a 16-bit autocast region on a ROCm device (the reference's
     ``fp16_run`` training, train_stft.py:165,216) this is the HIP training
@@ -443,9 +460,10 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) -> torch.T
     if wdt is None or not supported(module):
         if in_slope != 1.0:
             x = F.leaky_relu(x, in_slope)
-        return module(x)
+        return module(x) if residual is None else module(x) + residual
     w = weight_norm_effective(module)
-    return conv1d_hip(x, w, module.bias, module.dilation[0], module.padding[0], in_slope, wdt)
+    return conv1d_hip(x, w, module.bias, module.dilation[0], module.padding[0], in_slope, wdt,
+                      residual)
 
 
 # ---------------------------------------------------------------------------
