@@ -13,8 +13,9 @@ independent replicas of the same step; value = all output samples / the
 slowest rank's time ("scaling": "weak").
 
 Extra fields:
-  roofline      the dominant kernel (conv1d_mfma_kernel, every conv launch of
-                the step): algorithmic FLOPs / HIP-event-timed kernel time,
+  roofline      the dominant kernel (conv1d_mfma_kernel + the fused ResBlock2
+                pair kernel, every conv launch of the step): algorithmic FLOPs /
+                HIP-event-timed kernel time,
                 against the fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
   cpu_baseline  the CPU oracle (oracle/vits_oracle.py, torch fp32 CPU: the
                 reference algorithm restated) on a bounded sample.
@@ -122,7 +123,7 @@ def pmc_traffic():
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    c = d.get("conv1d_mfma_kernel", {})
+    c = d.get("conv_kernels", d.get("conv1d_mfma_kernel", {}))
     return c.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
@@ -479,7 +480,9 @@ def main():
             per_launch_flops = s["total_flops"] / max(1, s["launches"])
             achieved = (s["total_flops"] / 1e12) / (s["total_ms"] / 1e3)
             traffic, tsrc = pmc_traffic()
-            roof = {"bound": "mfma", "kernel": "conv1d_mfma_kernel (all conv launches of a step)",
+            roof = {"bound": "mfma",
+                    "kernel": "conv1d_mfma_kernel + resblock_pair_kernel (every conv / fused "
+                              "ResBlock2-pair launch of a step)",
                     "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",

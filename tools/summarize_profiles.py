@@ -30,7 +30,9 @@ fam = defaultdict(lambda: [0, 0.0])
 for r in stats:
     name = r["Name"]
     short = name.replace("(anonymous namespace)::", "").replace("void ", "")
-    key = "conv1d_mfma_kernel" if "conv1d_mfma_kernel" in name else short.split("(")[0].split("<")[0][:60]
+    key = ("conv1d_mfma_kernel" if "conv1d_mfma_kernel" in name else
+           "resblock_pair_kernel" if "resblock_pair_kernel" in name else
+           short.split("(")[0].split("<")[0][:60])
     fam[key][0] += int(r["Calls"])
     fam[key][1] += float(r["TotalDurationNs"])
 families = {k: {"calls": v[0], "total_ms": round(v[1] / 1e6, 3),
@@ -40,7 +42,10 @@ families = {k: {"calls": v[0], "total_ms": round(v[1] / 1e6, 3),
 
 def pmc(name):
     rows = list(csv.DictReader(open(os.path.join(src, name, "run_counter_collection.csv"))))
-    vals = [float(r["Counter_Value"]) for r in rows if "conv1d_mfma_kernel" in r["Kernel_Name"]]
+    # the bench's dominant kernel: every conv launch of the step (the conv
+    # kernel and the fused ResBlock2 pair kernel)
+    vals = [float(r["Counter_Value"]) for r in rows
+            if "conv1d_mfma_kernel" in r["Kernel_Name"] or "resblock_pair_kernel" in r["Kernel_Name"]]
     return vals
 
 
@@ -52,12 +57,13 @@ write_b = sum(write[:n]) * 1024 / n
 summary = {
     "tag": tag,
     "kernel_families": families,
-    "conv1d_mfma_kernel": {
+    "conv_kernels": {
+        "kernels": "conv1d_mfma_kernel + resblock_pair_kernel",
         "pmc_launches": n,
         "hbm_fetch_bytes_per_launch": round(fetch_b),
         "hbm_write_bytes_per_launch": round(write_b),
         "hbm_bytes_per_launch": round(fetch_b + write_b),
-        "note": "FETCH_SIZE x2 (gfx950 wide-read correction), KiB->B; averaged over every conv launch of 3 infer_p2 steps",
+        "note": "FETCH_SIZE x2 (gfx950 wide-read correction), KiB->B; averaged over every conv / fused-pair launch of the infer_p2 steps",
     },
 }
 with open(os.path.join(dst, f"{tag}_summary.json"), "w") as f:
