@@ -445,6 +445,63 @@ int vits_radam_step(const vits_radam_tensor* tensors, int n, float* scal, const 
                     const float* grad_scale, double lr, const double* lr_dev, double beta1,
                     double beta2, double eps, double weight_decay, void* stream);
 
+/* ---------------------------------------------------------------------- */
+/* Weight normalisation of many layers in one launch (legacy             */
+/* torch.nn.utils.weight_norm, dim 0: the generator's convs, upsamplers   */
+/* and conditioning Linears, modules.py:58-109, models.py:233; replaces   */
+/* the per-layer torch._weight_norm / its backward of every forward).     */
+/* Each layer is [rows][cols] (rows = size of dim 0), fp32, contiguous.  */
+/* forward: w = v * (g / ||v_row||), norms[row] written (global row      */
+/* index over all layers of the call, in order); backward (same layers,  */
+/* same norms): dg = <dw,v>/n, dv = (g/n)(dw - v <dw,v>/n^2).            */
+/* ---------------------------------------------------------------------- */
+#define VITS_WNORM_MAX 56
+typedef struct vits_wnorm_layer {
+  const float* v;
+  const float* g;
+  float* w;        /* forward output */
+  const float* dw; /* backward input */
+  float* dv;       /* backward outputs */
+  float* dg;
+  int32_t rows;
+  int32_t cols;
+} vits_wnorm_layer;
+int vits_weight_norm_forward(const vits_wnorm_layer* layers, int n, float* norms, void* stream);
+int vits_weight_norm_backward(const vits_wnorm_layer* layers, int n, const float* norms,
+                              void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* Spectral normalisation of many layers in one launch (torch.nn.utils.  */
+/* spectral_norm, dim 0, one power iteration per training forward, the   */
+/* discriminators of mrd.py; replaces the per-layer forward pre-hooks).  */
+/* forward (one workgroup per layer): training: v = normalize(W^T u),    */
+/* u = normalize(W v), u / v updated in place; sigma = u . (W v);        */
+/* w_sn = W / sigma; saved = [sigma, u (rows), v (cols)] of this call.   */
+/* backward: dw = dw_sn / sigma - (<dw_sn, W> / sigma^2) u v^T.          */
+/* emu16 = 1: the hook inside an fp16 autocast region (mv operands and   */
+/* result rounded to fp16, as the reference's autocast mv).              */
+/* A layer needs 4 * (2 rows + cols + 4) <= VITS_SNORM_MAX_LDS bytes.    */
+/* ---------------------------------------------------------------------- */
+#define VITS_SNORM_MAX 48
+#define VITS_SNORM_MAX_LDS 65536
+typedef struct vits_snorm_layer {
+  const float* w;     /* weight_orig viewed [rows][cols] */
+  float* u;           /* [rows] buffer */
+  float* v;           /* [cols] buffer */
+  float* w_sn;        /* forward output */
+  const float* dw_sn; /* backward input */
+  float* dw;          /* backward output */
+  float* saved;       /* [1 + rows + cols] */
+  int32_t rows;
+  int32_t cols;
+  float eps;
+  int32_t reserved;
+} vits_snorm_layer;
+int vits_spectral_norm_supported(int rows, int cols);
+int vits_spectral_norm_forward(const vits_snorm_layer* layers, int n, int training, int emu16,
+                               void* stream);
+int vits_spectral_norm_backward(const vits_snorm_layer* layers, int n, int emu16, void* stream);
+
 /* library introspection */
 const char* vits_amd_version(void);
 int vits_amd_device_arch(char* buf, int len);

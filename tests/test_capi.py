@@ -40,17 +40,19 @@ def test_struct_layout_matches_header():
     import subprocess
     import tempfile
 
-    from vits_amd._lib import ConvDesc, ConvOut, ResblockPairDesc, StftJob
+    from vits_amd._lib import (WNORM_MAX, SNORM_MAX, ConvDesc, ConvOut, ResblockPairDesc,
+                               SnormLayer, StftJob, WnormLayer)
 
     probe = r'''
 #include <stdio.h>
 #include <stddef.h>
 #include "vits_amd.h"
-int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc),
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d\n", sizeof(vits_conv1d_desc),
  sizeof(vits_conv_out), offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths),
  offsetof(vits_conv1d_desc, wdtype), sizeof(vits_stft_job), offsetof(vits_stft_job, eps),
  sizeof(vits_resblock_pair_desc), offsetof(vits_resblock_pair_desc, w2),
- offsetof(vits_resblock_pair_desc, post_div));
+ offsetof(vits_resblock_pair_desc, post_div), sizeof(vits_wnorm_layer),
+ sizeof(vits_snorm_layer), offsetof(vits_snorm_layer, eps), VITS_WNORM_MAX, VITS_SNORM_MAX);
  return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -70,3 +72,7 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vits_conv1
     assert int(out[7]) == ctypes.sizeof(ResblockPairDesc)
     assert int(out[8]) == ResblockPairDesc.w2.offset
     assert int(out[9]) == ResblockPairDesc.post_div.offset
+    assert int(out[10]) == ctypes.sizeof(WnormLayer)
+    assert int(out[11]) == ctypes.sizeof(SnormLayer)
+    assert int(out[12]) == SnormLayer.eps.offset
+    assert int(out[13]) == WNORM_MAX and int(out[14]) == SNORM_MAX

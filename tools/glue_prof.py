@@ -35,6 +35,19 @@ class Rec(TorchDispatchMode):
             if "/vits_amd/" in fr.filename:
                 where = f"{fr.filename.split('/vits_amd/')[-1]}:{fr.lineno} {fr.name}"
                 break
+        if where == "?":
+            # backward: the forward site of the autograd node being run
+            # (anomaly mode stores each node's forward traceback)
+            node = torch._C._current_autograd_node()
+            if node is not None:
+                tb = node.metadata.get("traceback_", [])
+                lines = tb if isinstance(tb, list) else str(tb).splitlines()
+                site = "?"
+                for ln in lines:
+                    ln = str(ln)
+                    if "/vits_amd/" in ln and "line" in ln:
+                        site = ln.strip().split("/vits_amd/")[-1].replace('", line ', ":")
+                where = f"bwd[{node.name()}] {site}"
         nbytes = 0
         for o in (out if isinstance(out, (tuple, list)) else (out,)):
             if isinstance(o, torch.Tensor):
@@ -48,6 +61,7 @@ class Rec(TorchDispatchMode):
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--top", type=int, default=70)
+ap.add_argument("--by", choices=("bytes", "count"), default="bytes")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 hps = default_hps()
@@ -58,10 +72,11 @@ batch = [t.to(dev) for t in synthetic_batch(hps, args.batch, seed=0)]
 st.step(batch)
 torch.cuda.synchronize()
 rec = Rec()
-with rec:
+with rec, torch.autograd.detect_anomaly(check_nan=False):
     st.step(batch)
 torch.cuda.synchronize()
 tot = sum(v[0] for v in rec.agg.values())
 print(f"ops {sum(v[1] for v in rec.agg.values())}, bytes written {tot / 2**20:.1f} MiB")
-for (name, where), (b, n) in sorted(rec.agg.items(), key=lambda kv: -kv[1][0])[:args.top]:
+key = 0 if args.by == "bytes" else 1
+for (name, where), (b, n) in sorted(rec.agg.items(), key=lambda kv: -kv[1][key])[:args.top]:
     print(f"{b / 2**20:9.1f} MiB {n:5d}  {name:40s} {where}")

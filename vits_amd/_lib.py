@@ -174,6 +174,39 @@ class RadamTensor(C.Structure):
     ]
 
 
+WNORM_MAX = 56
+SNORM_MAX = 48
+
+
+class WnormLayer(C.Structure):
+    _fields_ = [
+        ("v", C.c_void_p),
+        ("g", C.c_void_p),
+        ("w", C.c_void_p),
+        ("dw", C.c_void_p),
+        ("dv", C.c_void_p),
+        ("dg", C.c_void_p),
+        ("rows", C.c_int32),
+        ("cols", C.c_int32),
+    ]
+
+
+class SnormLayer(C.Structure):
+    _fields_ = [
+        ("w", C.c_void_p),
+        ("u", C.c_void_p),
+        ("v", C.c_void_p),
+        ("w_sn", C.c_void_p),
+        ("dw_sn", C.c_void_p),
+        ("dw", C.c_void_p),
+        ("saved", C.c_void_p),
+        ("rows", C.c_int32),
+        ("cols", C.c_int32),
+        ("eps", C.c_float),
+        ("reserved", C.c_int32),
+    ]
+
+
 _SIGS = {
     "vits_conv1d_forward": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_void_p]),
     "vits_conv1d_forward_seq": (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.c_int, C.c_void_p]),
@@ -279,6 +312,15 @@ _SIGS = {
         [C.POINTER(RadamTensor), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
          C.c_void_p] + [C.c_double] * 4 + [C.c_void_p],
     ),
+    "vits_weight_norm_forward": (
+        C.c_int, [C.POINTER(WnormLayer), C.c_int, C.c_void_p, C.c_void_p]),
+    "vits_weight_norm_backward": (
+        C.c_int, [C.POINTER(WnormLayer), C.c_int, C.c_void_p, C.c_void_p]),
+    "vits_spectral_norm_supported": (C.c_int, [C.c_int, C.c_int]),
+    "vits_spectral_norm_forward": (
+        C.c_int, [C.POINTER(SnormLayer), C.c_int, C.c_int, C.c_int, C.c_void_p]),
+    "vits_spectral_norm_backward": (
+        C.c_int, [C.POINTER(SnormLayer), C.c_int, C.c_int, C.c_void_p]),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
 }

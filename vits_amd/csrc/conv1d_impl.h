@@ -7,6 +7,12 @@
 
 #include "common.h"
 
+#ifdef VITS_NOPRIO
+#define VITS_PRIO(x) ((void)0)
+#else
+#define VITS_PRIO(x) __builtin_amdgcn_s_setprio(x)
+#endif
+
 namespace vits_conv {
 
 
@@ -388,25 +394,25 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   #pragma unroll
         for (int ni = 0; ni < TN; ++ni) b1[ni] = pb[ni * 32];
         advance();
-        __builtin_amdgcn_s_setprio(1);
+        VITS_PRIO(1);
   #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
   #pragma unroll
           for (int ni = 0; ni < TN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        VITS_PRIO(0);
   #pragma unroll
         for (int mi = 0; mi < TM; ++mi) a0[mi] = pa[mi * 32];
   #pragma unroll
         for (int ni = 0; ni < TN; ++ni) b0[ni] = pb[ni * 32];
         advance();
-        __builtin_amdgcn_s_setprio(1);
+        VITS_PRIO(1);
   #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
   #pragma unroll
           for (int ni = 0; ni < TN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[mi], b1[ni], acc[mi][ni], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        VITS_PRIO(0);
       }
       if (s < steps) {
   #pragma unroll

@@ -19,7 +19,7 @@ from torch.nn import Conv1d, Conv2d, LeakyReLU
 from torch.nn.utils import spectral_norm, weight_norm
 from torch.nn.utils.spectral_norm import SpectralNorm
 
-from . import train_ops
+from . import train_ops, wnorm
 from .commons import get_padding
 
 LRELU_SLOPE = 0.2
@@ -202,8 +202,34 @@ class GroupedSpectralNorm:
                     del m._forward_pre_hooks[k]
                     key = (tuple(getattr(m, hook.name + "_orig").shape), hook.eps, hook.name)
                     self.groups.setdefault(key, []).append(m)
+        self.flat = [(m, name, eps) for (_, eps, name), mods in self.groups.items() for m in mods]
+        self._fused = None
+
+    def _fused_ok(self) -> bool:
+        """All layers on the one-launch HIP path (wnorm.spectral_norm_all):
+        CUDA fp32 weights within its LDS budget, autocast off or fp16."""
+        if not (wnorm.FUSED_NORMS and wnorm.FUSED_SN and self.flat):
+            return False
+        dev = getattr(self.flat[0][0], self.flat[0][1] + "_orig").device
+        if dev.type != "cuda":
+            return False
+        if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") != torch.float16:
+            return False
+        if self._fused is None:
+            self._fused = all(
+                wnorm.spectral_norm_supported(getattr(m, n + "_orig"))
+                and getattr(m, n + "_u").dtype == torch.float32
+                and getattr(m, n + "_v").dtype == torch.float32
+                for m, n, _ in self.flat)
+        return self._fused
 
     def apply(self, training: bool):
+        if self._fused_ok():
+            Ws = [getattr(m, n + "_orig") for m, n, _ in self.flat]
+            layers = [(getattr(m, n + "_u"), getattr(m, n + "_v"), eps) for m, n, eps in self.flat]
+            for (m, n, _), w in zip(self.flat, wnorm.spectral_norm_all(Ws, layers, training)):
+                setattr(m, n, w)
+            return
         for (shape, eps, name), mods in self.groups.items():
             W = torch.stack([getattr(m, name + "_orig") for m in mods])  # [G, out, ...]
             G, h = W.shape[0], W.shape[1]

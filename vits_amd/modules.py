@@ -73,7 +73,7 @@ class WN(nn.Module):
         H = self.hidden_channels
         output = torch.zeros_like(x)
         if self.gin_channels != 0:
-            g = self.cond_layer(g)
+            g = train_ops.linear(self.cond_layer, g)
         for i in range(self.n_layers):
             x_in = train_ops.conv1d(self.in_layers[i], x)
             acts = self.drop(self._gate(x_in, g if self.gin_channels else None, i))
@@ -117,7 +117,7 @@ class ResBlock2(nn.Module):
             return resblock_infer(self, x, g)
         for c1, c2, cs in zip(self.convs1, self.convs2, self.conds):
             xt = train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE)
-            xt = train_ops.gate(xt, cs(g))
+            xt = train_ops.gate(xt, train_ops.linear(cs, g))
             # modules.py:258-259 (xt = c2(xt); x = xt + x): the add in the
             # conv epilogue on the fp16 training path
             x = train_ops.conv1d(c2, xt, residual=x)

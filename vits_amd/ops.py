@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes as C
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import Optional
@@ -44,8 +45,27 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+_WEIGHT_CACHE: dict = {}
+
+
+def set_weight_cache(cache: dict) -> dict:
+    """Install ``{module: effective weight}`` (wnorm.WeightNormCache.active:
+    every weight-normed layer of a network computed in one launch); returns
+    the previous mapping."""
+    global _WEIGHT_CACHE
+    prev, _WEIGHT_CACHE = _WEIGHT_CACHE, cache
+    return prev
+
+
+def cached_weight(module: torch.nn.Module):
+    return _WEIGHT_CACHE.get(module)
+
+
 def weight_norm_effective(module: torch.nn.Module, name: str = "weight") -> torch.Tensor:
     """Effective weight of a (legacy) weight-normed or plain layer."""
+    w = _WEIGHT_CACHE.get(module) if name == "weight" else None
+    if w is not None:
+        return w
     g = getattr(module, name + "_g", None)
     v = getattr(module, name + "_v", None)
     if g is not None and v is not None:
@@ -95,6 +115,10 @@ X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::
 # 64x128 89 -> 5; 64x256 is budgeted at 3: its k=7 convs run faster with the
 # bigger chunk); the K-chunk is sized so that LDS does not cut this further
 TILE_OCCUPANCY = {TILE_128x128: 3, TILE_64x256: 3, TILE_32x256: 4, TILE_64x128: 5}
+# experiment knob (tools/ab_*.sh): VITS_TILE_OCC="tile:wgs,..." overrides entries
+for _kv in filter(None, os.environ.get("VITS_TILE_OCC", "").split(",")):
+    _t, _o = _kv.split(":")
+    TILE_OCCUPANCY[int(_t)] = int(_o)
 LDS_BYTES_PER_CU = 160 * 1024
 
 
@@ -358,6 +382,7 @@ class ConvTimer:
 
     def __init__(self):
         self.records = []  # (start_event, end_event, flops)
+        self.shapes = []   # one label per record (tools/infer_breakdown.py)
 
     def __enter__(self):
         ConvTimer.active = self
@@ -380,6 +405,8 @@ class ConvTimer:
               "vits_conv1d_forward_groups")
         e.record(stream)
         self.records.append((s, e, sum(conv_flops(d, batch) for d in group)))
+        self.shapes.append("conv " + "+".join(
+            f"m{d.m}c{d.cin}k{d.k}d{d.dil}T{d.n_out}e{d.epi}t{d.tile}" for d in group))
 
     def launch_pairs(self, lib, group, batch, device):
         s = torch.cuda.Event(enable_timing=True)
@@ -391,6 +418,8 @@ class ConvTimer:
               "vits_resblock_pair_forward")
         e.record(stream)
         self.records.append((s, e, sum(resblock_pair_flops(d, batch) for d in group)))
+        self.shapes.append("pair " + "+".join(
+            f"C{d.channels}k{d.k}d{d.dil}T{d.t_len}" for d in group))
 
     def summary(self):
         torch.cuda.synchronize()
@@ -398,6 +427,12 @@ class ConvTimer:
         fl = [f for _, _, f in self.records]
         return dict(launches=len(ms), total_ms=float(sum(ms)), total_flops=int(sum(fl)),
                     avg_ms=float(sum(ms) / max(1, len(ms))))
+
+    def per_launch(self):
+        """[(label, ms, flops)] in launch order."""
+        torch.cuda.synchronize()
+        return [(lab, s.elapsed_time(e), f)
+                for lab, (s, e, f) in zip(self.shapes, self.records)]
 
 
 # ---------------------------------------------------------------------------

@@ -38,6 +38,7 @@ from .mel_processing import mel_spectrogram_torch, spec_to_mel_torch
 from .models import MultiPeriodDiscriminator, SynthesizerTrn
 from .optim import FusedRAdam, RAdam
 from .stft_loss import MultiResolutionSTFTLoss
+from .wnorm import WeightNormCache
 
 
 def build_models(hps, device, variant: str = "stft"):
@@ -119,6 +120,9 @@ class TrainStep:
                     for t in list(net.parameters()) + list(net.buffers()):
                         dist.broadcast(t, src=0)
         self.net_g, self.net_d = net_g, net_d
+        # every weight-normed generator layer in one launch each way (GPU)
+        self._wn_g = (WeightNormCache(net_g.module if isinstance(net_g, DDP) else net_g)
+                      if device.type == "cuda" else None)
         fp16 = bool(hps.train.fp16_run) and device.type == "cuda"
         # the autocast weight-cast cache must be off under graph capture (cached
         # fp16 weight copies would outlive / escape the captured region)
@@ -126,6 +130,9 @@ class TrainStep:
         self.autocast = lambda enabled=fp16: torch.autocast(device.type, dtype=torch.float16,
                                                             enabled=enabled, cache_enabled=cache)
         self.scaler = torch.amp.GradScaler(device.type, enabled=fp16)
+
+    def _g_weights(self):
+        return self._wn_g.active() if self._wn_g is not None else contextlib.nullcontext()
 
     def end_epoch(self):
         """The per-epoch lr decay of train_stft.py:138-139; reaches a captured
@@ -141,7 +148,7 @@ class TrainStep:
         x, x_lengths, spec, spec_lengths, y, y_lengths, emo, speakers = (
             t.to(self.device, non_blocking=True) for t in batch)
         with self.autocast():
-            with rf("step:G.forward"):
+            with rf("step:G.forward"), self._g_weights():
                 (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
                  (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
                     x, x_lengths, spec, spec_lengths, emo, speakers)
@@ -224,7 +231,7 @@ class TrainStep:
             t.to(self.device, non_blocking=True) for t in batch)
         seg = hps.train.segment_size // hps.data.hop_length
         with self.autocast():
-            with rf("step:G.forward"):
+            with rf("step:G.forward"), self._g_weights():
                 (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
                  (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
                     x, x_lengths, spec, spec_lengths, emo, speakers)

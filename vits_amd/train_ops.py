@@ -40,8 +40,8 @@ from torch import nn
 
 from . import _lib
 from ._lib import EPI_STORE, TILE_64x128, TILE_128x128, WDT_BF16, WDT_F16, ConvWgradDesc, check
-from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, conv1d_launch, make_desc, make_out,
-                  weight_norm_effective)
+from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
+                  make_desc, make_out, weight_norm_effective)
 
 _TORCH_16 = {WDT_F16: torch.float16, WDT_BF16: torch.bfloat16}
 TRAIN_WDTYPE = WDT_F16  # the reference's autocast dtype (train_stft.py:165)
@@ -443,6 +443,20 @@ def autocast_wdtype(device_type: str = "cuda"):
         return None
     dt = torch.get_autocast_dtype(device_type)
     return {torch.float16: WDT_F16, torch.bfloat16: WDT_BF16}.get(dt)
+
+
+def linear(module: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """``module(x)`` for an nn.Linear / 1x1 nn.Conv1d (the conditioning
+    layers, modules.py:76,120), with the weight of the active weight-norm
+    cache (wnorm.WeightNormCache) when there is one; the module's own
+    (hooked) forward otherwise."""
+    w = cached_weight(module)
+    if w is None:
+        return module(x)
+    if isinstance(module, nn.Conv1d):
+        return F.conv1d(x, w, module.bias, module.stride, module.padding, module.dilation,
+                        module.groups)
+    return F.linear(x, w, module.bias)
 
 
 def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0,
