@@ -471,19 +471,18 @@ int vits_weight_norm_backward(const vits_wnorm_layer* layers, int n, const float
                               void* stream);
 
 /* ---------------------------------------------------------------------- */
-/* Spectral normalisation of many layers in one launch (torch.nn.utils.  */
+/* Spectral normalisation of many layers at once (torch.nn.utils.        */
 /* spectral_norm, dim 0, one power iteration per training forward, the   */
 /* discriminators of mrd.py; replaces the per-layer forward pre-hooks).  */
-/* forward (one workgroup per layer): training: v = normalize(W^T u),    */
+/* forward (5 launches for all layers): training: v = normalize(W^T u),  */
 /* u = normalize(W v), u / v updated in place; sigma = u . (W v);        */
 /* w_sn = W / sigma; saved = [sigma, u (rows), v (cols)] of this call.   */
-/* backward: dw = dw_sn / sigma - (<dw_sn, W> / sigma^2) u v^T.          */
+/* backward (2 launches): dw = dw_sn / sigma - (<dw_sn, W> / sigma^2)    */
+/* u v^T, with a workspace of vits_spectral_norm_workspace floats.       */
 /* emu16 = 1: the hook inside an fp16 autocast region (mv operands and   */
 /* result rounded to fp16, as the reference's autocast mv).              */
-/* A layer needs 4 * (2 rows + cols + 4) <= VITS_SNORM_MAX_LDS bytes.    */
 /* ---------------------------------------------------------------------- */
 #define VITS_SNORM_MAX 48
-#define VITS_SNORM_MAX_LDS 65536
 typedef struct vits_snorm_layer {
   const float* w;     /* weight_orig viewed [rows][cols] */
   float* u;           /* [rows] buffer */
@@ -500,7 +499,9 @@ typedef struct vits_snorm_layer {
 int vits_spectral_norm_supported(int rows, int cols);
 int vits_spectral_norm_forward(const vits_snorm_layer* layers, int n, int training, int emu16,
                                void* stream);
-int vits_spectral_norm_backward(const vits_snorm_layer* layers, int n, int emu16, void* stream);
+int64_t vits_spectral_norm_workspace(const vits_snorm_layer* layers, int n);
+int vits_spectral_norm_backward(const vits_snorm_layer* layers, int n, int emu16,
+                                float* workspace, int64_t ws_floats, void* stream);
 
 /* library introspection */
 const char* vits_amd_version(void);

@@ -246,15 +246,34 @@ class Generator(nn.Module):
             # inference: HIP plan only (raises off-GPU; there is no CPU path)
             return engine.generator_forward(self, x, g)
         x = train_ops.conv1d(self.conv_pre, x)
+        conds = self._resblock_conds(g)
         for i in range(self.num_upsamples):
             # polyphase on the HIP training conv under autocast (torch otherwise)
             x = train_ops.conv_transpose1d(self.ups[i], x, in_slope=modules.LRELU_SLOPE)
             xs = 0
             for j in range(self.num_kernels):
-                xs = xs + self.resblocks[i * self.num_kernels + j](x, g=g)
+                rb = i * self.num_kernels + j
+                xs = xs + self.resblocks[rb](x, g=g, conds=None if conds is None else conds[rb])
             x = xs / self.num_kernels
         x = train_ops.conv1d(self.conv_post, x, in_slope=0.01)  # F.leaky_relu default slope
         return torch.tanh(x)
+
+    def _resblock_conds(self, g):
+        """Every ResBlock2 conditioning Linear (modules.py:250-255: one per
+        dilation pair, 36 at the base config, all applied to the same g) as
+        ONE GEMM over the concatenated weights, split back per resblock:
+        the same products, one launch instead of 36 (each with its own
+        autocast casts and backward GEMMs).  None without a speaker vector."""
+        if g is None or not g.is_cuda:
+            return None
+        mods = [cs for rb in self.resblocks for cs in rb.conds]
+        if not all(isinstance(m, nn.Linear) and m.bias is not None for m in mods):
+            return None
+        ws = [train_ops.module_weight(m) for m in mods]
+        y = F.linear(g, torch.cat(ws, 0), torch.cat([m.bias for m in mods]))
+        parts = torch.split(y, [w.shape[0] for w in ws], dim=1)
+        k = len(self.resblocks[0].conds)
+        return [parts[i * k:(i + 1) * k] for i in range(len(self.resblocks))]
 
     def infer(self, x, g):
         return self.forward(x, g)

@@ -109,15 +109,17 @@ class ResBlock2(nn.Module):
             weight_norm(nn.Linear(gin_channels, inter)) for _ in dilation])
         self.apply(init_weights)
 
-    def forward(self, x, g=None):
+    def forward(self, x, g=None, conds=None):
+        """conds: the conditioning Linears' outputs when the caller computed
+        them (Generator._resblock_conds: all resblocks in one GEMM)."""
         if not (torch.is_grad_enabled() and (x.requires_grad or any(
                 p.requires_grad for p in self.parameters()))):
             from .engine import resblock_infer
 
             return resblock_infer(self, x, g)
-        for c1, c2, cs in zip(self.convs1, self.convs2, self.conds):
+        for i, (c1, c2, cs) in enumerate(zip(self.convs1, self.convs2, self.conds)):
             xt = train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE)
-            xt = train_ops.gate(xt, train_ops.linear(cs, g))
+            xt = train_ops.gate(xt, train_ops.linear(cs, g) if conds is None else conds[i])
             # modules.py:258-259 (xt = c2(xt); x = xt + x): the add in the
             # conv epilogue on the fp16 training path
             x = train_ops.conv1d(c2, xt, residual=x)

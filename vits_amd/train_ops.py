@@ -445,6 +445,13 @@ def autocast_wdtype(device_type: str = "cuda"):
     return {torch.float16: WDT_F16, torch.bfloat16: WDT_BF16}.get(dt)
 
 
+def module_weight(module: nn.Module) -> torch.Tensor:
+    """A layer's effective weight: the active weight-norm cache's, or the
+    weight-norm / plain weight computed here."""
+    w = cached_weight(module)
+    return w if w is not None else weight_norm_effective(module)
+
+
 def linear(module: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """``module(x)`` for an nn.Linear / 1x1 nn.Conv1d (the conditioning
     layers, modules.py:76,120), with the weight of the active weight-norm

@@ -195,8 +195,11 @@ class _SpectralNormAll(torch.autograd.Function):
                 e.w, e.dw_sn, e.dw = Ws[i].data_ptr(), g.data_ptr(), dWs[i].data_ptr()
                 e.saved = saved.data_ptr() + 4 * ctx.offs[i]
                 e.rows, e.cols = ctx.shapes[i]
-            check(_lib.load().vits_spectral_norm_backward(arr, len(idx), int(ctx.emu16),
-                                                          _stream(saved)),
+            lib = _lib.load()
+            nws = lib.vits_spectral_norm_workspace(arr, len(idx))
+            ws = torch.empty(max(1, nws), device=saved.device, dtype=torch.float32)
+            check(lib.vits_spectral_norm_backward(arr, len(idx), int(ctx.emu16), ws.data_ptr(),
+                                                  ws.numel(), _stream(saved)),
                   "vits_spectral_norm_backward")
         return (None, None, None, *dWs)
 
