@@ -37,7 +37,10 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   VITS_CHECK_SHAPE(d.tin >= 0 && d.x_tstride >= 1);
   VITS_CHECK_SHAPE(d.x_tstride != 1 || d.x_cstride >= d.tin);
   if (d.epi == VITS_EPI_GATE) VITS_CHECK_SHAPE((d.m % 2) == 0);
-  if (d.epi == VITS_EPI_UPSAMPLE) VITS_CHECK_SHAPE(d.up_u > 0 && d.m % d.up_u == 0 && d.t_out > 0);
+  // (the epilogue's fp32 row / u is exact for rows < 2^14, u <= 64)
+  if (d.epi == VITS_EPI_UPSAMPLE)
+    VITS_CHECK_SHAPE(d.up_u > 0 && d.up_u <= 64 && d.m < (1 << 14) && d.m % d.up_u == 0 &&
+                     d.t_out > 0);
   if (d.epi == VITS_EPI_STORE && d.split < d.m) VITS_CHECK_ARG(d.out1.y != nullptr);
   if ((reinterpret_cast<uintptr_t>(d.w) & 15) != 0) return VITS_E_SHAPE;
   VITS_CHECK_ARG(d.wdtype == VITS_WDT_F32 || d.wdtype == VITS_WDT_BF16 ||

@@ -475,12 +475,17 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
         }
       } else if (EPI == VITS_EPI_UPSAMPLE) {
         const int u = p.up_u;
+        // row / u without the integer-division sequence per element:
+        // (row + 0.5) / u lies >= 0.5/u from an integer, and for rows < 2^14
+        // and u <= 64 (checked on the host) the fp32 product's error is
+        // below that, so its floor is exact
+        const float inv_u = 1.0f / (float)u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ro = (r & 3) + 8 * (r >> 2);
           const int row = rbase + ro;
           if (row < p.m && n < p.n_out) {
-            const int oc = row / u;
+            const int oc = (int)(((float)row + 0.5f) * inv_u);
             const int ph = row - oc * u;
             const int t = n * u + ph - p.up_pad;
             if (t >= 0 && t < p.t_out) {
