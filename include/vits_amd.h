@@ -503,6 +503,22 @@ int64_t vits_spectral_norm_workspace(const vits_snorm_layer* layers, int n);
 int vits_spectral_norm_backward(const vits_snorm_layer* layers, int n, int emu16,
                                 float* workspace, int64_t ws_floats, void* stream);
 
+/* ---------------------------------------------------------------------- */
+/* The residual / skip update between two WN layers of the fp16-autocast  */
+/* training step (modules.py:93-182): x' = (x + rs[:, :H]) * mask (fp32), */
+/* x16' = x' rounded to the 16-bit type (the next conv's input), out' =   */
+/* out + rs[:, H:] (out NULL = 0); rs [B][2H][T] of the 16-bit type, x /  */
+/* out / x' / out' [B][H][T] fp32, mask [B][1][T] fp32, all contiguous.   */
+/* backward: G = dx' + dx16' (either NULL = 0), dx = G * mask, drs =      */
+/* [G * mask ; dout'] rounded to the 16-bit type (dout' NULL = 0).        */
+/* ---------------------------------------------------------------------- */
+int vits_wn_update_forward(const float* x, const void* rs, const float* mask, const float* out,
+                           float* x_new, void* x16_new, float* out_new, int batch, int H, int T,
+                           int wdtype, void* stream);
+int vits_wn_update_backward(const float* gx, const void* gx16, const float* gout,
+                            const float* mask, float* dx, void* drs, int batch, int H, int T,
+                            int wdtype, void* stream);
+
 /* library introspection */
 const char* vits_amd_version(void);
 int vits_amd_device_arch(char* buf, int len);

@@ -346,3 +346,44 @@ def test_conv1d_train_io16_residual(device):
     _close(rd.grad, rr.grad, "dres", tol=0)
     _close(xd.grad, xr.grad, "dx", tol=TOL16)
     _close(wd.grad, wr.grad, "dw")
+
+
+@pytest.mark.parametrize("with_out", [True, False])
+def test_wn_update_matches_torch(with_out):
+    """WNUpdate16 (csrc/wnres.hip) vs the reference's torch ops of WN.forward
+    (modules.py:93-182) under fp16 autocast: x' = (x + rs[:, :H]) * mask,
+    out' = out + rs[:, H:], x16' = x'.half(); forward and every gradient
+    bit-exact (same fp32 / fp16 roundings, element-wise)."""
+    dev = torch.device("cuda:0")
+    B, H, T = 3, 192, 157
+    gen = torch.Generator(device=dev).manual_seed(4)
+    x = torch.randn(B, H, T, device=dev, generator=gen)
+    rs = torch.randn(B, 2 * H, T, device=dev, generator=gen).half()
+    mask = torch.ones(B, 1, T, device=dev)
+    mask[1, :, 100:] = 0
+    out = torch.randn(B, H, T, device=dev, generator=gen) if with_out else None
+    a = torch.randn(B, H, T, device=dev, generator=gen)
+    b16 = torch.randn(B, H, T, device=dev, generator=gen).half()
+    c = torch.randn(B, H, T, device=dev, generator=gen)
+
+    def run(fused):
+        xs = x.clone().requires_grad_()
+        rss = rs.clone().requires_grad_()
+        outs = None if out is None else out.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.float16):
+            if fused:
+                xn, x16, on = train_ops.wn_update(xs, rss, mask, outs)
+            else:
+                xn = (xs + rss[:, :H]) * mask
+                on = (torch.zeros_like(xs) if outs is None else outs) + rss[:, H:]
+                x16 = xn.half()
+        loss = (xn * a).sum() + (x16 * b16).float().sum() + (on * c).sum()
+        leaves = [xs, rss] + ([] if outs is None else [outs])
+        grads = torch.autograd.grad(loss, leaves)
+        return [xn, x16, on] + list(grads)
+
+    assert train_ops.TRAIN_IO16
+    got, want = run(True), run(False)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g.dtype == w.dtype and g.shape == w.shape, i
+        assert torch.equal(g, w), (i, (g.float() - w.float()).abs().max().item())

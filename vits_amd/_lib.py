@@ -322,6 +322,10 @@ _SIGS = {
     "vits_spectral_norm_workspace": (C.c_int64, [C.POINTER(SnormLayer), C.c_int]),
     "vits_spectral_norm_backward": (
         C.c_int, [C.POINTER(SnormLayer), C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),
+    "vits_wn_update_forward": (
+        C.c_int, [C.c_void_p] * 7 + [C.c_int] * 4 + [C.c_void_p]),
+    "vits_wn_update_backward": (
+        C.c_int, [C.c_void_p] * 6 + [C.c_int] * 4 + [C.c_void_p]),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
 }

@@ -71,18 +71,26 @@ class WN(nn.Module):
 
     def forward(self, x, x_mask, g=None, **kwargs):
         H = self.hidden_channels
-        output = torch.zeros_like(x)
+        output = None  # zeros_like(x), materialised on first use
         if self.gin_channels != 0:
             g = train_ops.linear(self.cond_layer, g)
+        x16 = None  # x rounded to the conv dtype by the fused update (WNUpdate16)
         for i in range(self.n_layers):
-            x_in = train_ops.conv1d(self.in_layers[i], x)
+            x_in = train_ops.conv1d(self.in_layers[i], x if x16 is None else x16)
             acts = self.drop(self._gate(x_in, g if self.gin_channels else None, i))
             rs = train_ops.conv1d(self.res_skip_layers[i], acts)
             if i < self.n_layers - 1:
-                x = (x + rs[:, :H]) * x_mask
-                output = output + rs[:, H:]
+                # x = (x + rs[:, :H]) * x_mask ; output = output + rs[:, H:]
+                # (one kernel each way on the fp16 training path)
+                upd = train_ops.wn_update(x, rs, x_mask, output)
+                if upd is not None:
+                    x, x16, output = upd
+                else:
+                    x16 = None
+                    x = (x + rs[:, :H]) * x_mask
+                    output = (torch.zeros_like(x) if output is None else output) + rs[:, H:]
             else:
-                output = output + rs
+                output = (torch.zeros_like(x) if output is None else output) + rs
         return output * x_mask
 
     def infer(self, x, g=None, **kwargs):

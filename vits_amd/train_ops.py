@@ -384,6 +384,56 @@ class GateHip16(torch.autograd.Function):
         return dx, (None if dg is None else dg.to(g.dtype)), None
 
 
+class WNUpdate16(torch.autograd.Function):
+    """x' = (x + rs[:, :H]) * mask, x16' = x' in the 16-bit type, out' = out +
+    rs[:, H:] (modules.WN between two layers, modules.py:93-182) - one
+    kernel each way (csrc/wnres.hip).  out may be None (= 0)."""
+
+    @staticmethod
+    def forward(ctx, x, rs, mask, out, wdtype: int):
+        B, H, T = x.shape
+        assert rs.shape == (B, 2 * H, T) and mask.shape == (B, 1, T)
+        xn = torch.empty_like(x)
+        x16 = torch.empty(B, H, T, device=x.device, dtype=rs.dtype)
+        outn = torch.empty_like(x)
+        check(_lib.load().vits_wn_update_forward(
+            x.data_ptr(), rs.data_ptr(), mask.data_ptr(), None if out is None else out.data_ptr(),
+            xn.data_ptr(), x16.data_ptr(), outn.data_ptr(), B, H, T, wdtype,
+            _stream_ptr(x.device)), "vits_wn_update_forward")
+        ctx.save_for_backward(mask)
+        ctx.conf = (B, H, T, wdtype, rs.dtype, out is not None)
+        ctx.set_materialize_grads(False)
+        return xn, x16, outn
+
+    @staticmethod
+    def backward(ctx, gxn, gx16, gout):
+        (mask,) = ctx.saved_tensors
+        B, H, T, wdtype, dt, has_out = ctx.conf
+        dx = torch.empty(B, H, T, device=mask.device, dtype=torch.float32)
+        drs = torch.empty(B, 2 * H, T, device=mask.device, dtype=dt)
+        gxn = None if gxn is None else gxn.contiguous()
+        gx16 = None if gx16 is None else gx16.to(dt).contiguous()
+        gout = None if gout is None else gout.float().contiguous()
+        check(_lib.load().vits_wn_update_backward(
+            None if gxn is None else gxn.data_ptr(), None if gx16 is None else gx16.data_ptr(),
+            None if gout is None else gout.data_ptr(), mask.data_ptr(), dx.data_ptr(),
+            drs.data_ptr(), B, H, T, wdtype, _stream_ptr(mask.device)), "vits_wn_update_backward")
+        return dx, drs, None, (gout if has_out else None), None
+
+
+def wn_update(x: torch.Tensor, rs: torch.Tensor, mask: torch.Tensor, out):
+    """(x', x16', out') of WN's residual / skip update (WNUpdate16) when it
+    applies: an fp16-autocast training step on the GPU, fp32 contiguous x /
+    out / mask and a 16-bit rs; None otherwise (the caller runs torch)."""
+    wdt = autocast_wdtype() if x.device.type == "cuda" else None
+    if (wdt is None or not _io16(wdt) or rs.dtype != _TORCH_16[wdt] or x.dtype != torch.float32
+            or mask.dtype != torch.float32 or not x.is_contiguous() or not rs.is_contiguous()
+            or not mask.is_contiguous() or (out is not None and (out.dtype != torch.float32
+                                                                 or not out.is_contiguous()))):
+        return None
+    return WNUpdate16.apply(x, rs, mask, out, wdt)
+
+
 # 16-bit activations for the training convs / gates under fp16 autocast (the
 # reference's autocast convs return fp16); False: the fp32-I/O kernels
 TRAIN_IO16 = os.environ.get("VITS_TRAIN_IO16", "1") != "0"
