@@ -73,10 +73,13 @@ constexpr int VITS_W_TILE = 4096;
 // owned by thread i % 256; its (row, column) -> global offset mapping does
 // not depend on the chunk, so it is computed once per workgroup.  The host
 // keeps kc * xw_pad <= floats.
-template <int BN, bool BF = false>
+template <int BN, bool BF = false, bool IO16 = false>
 struct XTile {
-  // bf16-MFMA chunks carry >= 16 channels: a wider window budget
-  static constexpr int floats = BF ? (BN <= 128 ? 3072 : 5120) : (BN <= 128 ? 2048 : 4096);
+  // bf16-MFMA chunks carry >= 16 channels: a wider window budget; 16-bit
+  // activations (IO16) stage 2 bytes per element, so twice the elements fit
+  // the same registers (the training convs' 32- / 64-channel chunks)
+  static constexpr int floats = IO16 ? (BN <= 128 ? 6144 : 10240)
+                                     : BF ? (BN <= 128 ? 3072 : 5120) : (BN <= 128 ? 2048 : 4096);
   static constexpr int regs = floats / 256;
 };
 // bf16 W stage budget in float slots (2 bf16 each): k=11, kc=16, BM=64 fits
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   const int xstart = n0 - p.pad_left - xsh;  // V4: a multiple of 4
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
-  constexpr int MAXX = XTile<BN, BF>::regs;
+  constexpr int MAXX = XTile<BN, BF, IO16>::regs;
   constexpr int NU = V4 ? MAXX / 4 : MAXX;  // staging units per thread (blocks or elements)
   constexpr int UW = V4 ? 4 : 1;            // elements per unit
   typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -212,17 +215,27 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
     // the chunk's W image is R rows of L float slots, HBM row stride S:
     //   f32:  [kc*k][BM] rows of W[c][j][m0..m0+BM)
     //   bf16: [k*kc/8][BM*8 bf16] rows of W[chunk][j][c8][m0..m0+BM][8]
+    //   the packed image is [cin_pad/16][k][2][m_pad][8] (16-channel slabs)
+    //   and a chunk of kc = 16 s channels is s slabs: LDS row (j, c8) of the
+    //   [k][kc/8][BM][8] chunk image comes from slab c8/2, tap j, half c8&1
     const int L = BF ? BM * 4 : BM;
-    const float* wsrc = BF ? p.w + ((int64_t)(c0 / kc) * (k * (kc / 8)) * p.m_pad + m0) * 4
+    const float* wsrc = BF ? p.w + ((int64_t)(c0 / 16) * k * 2 * p.m_pad + m0) * 4
                            : p.w + (int64_t)c0 * k * p.m_pad + m0;
     const int64_t S = BF ? (int64_t)p.m_pad * 4 : p.m_pad;
+    const int c8n = kc >> 3;
     const int pieces = (wsz + 255) >> 8;
     for (int q = wid; q < pieces; q += 4) {
       const int e = q * 256 + lane * 4;
       if (e < wsz) {
         const int r = e / L;
         const int col = e - r * L;
-        __builtin_amdgcn_global_load_lds(wsrc + (int64_t)r * S + col,
+        int gr = r;
+        if (BF) {
+          const int j = r / c8n;
+          const int c8 = r - j * c8n;
+          gr = ((c8 >> 1) * k + j) * 2 + (c8 & 1);
+        }
+        __builtin_amdgcn_global_load_lds(wsrc + (int64_t)gr * S + col,
                                          (lds_void_t)(st + q * 256), 16, 0, 0);
       }
     }
@@ -579,7 +592,8 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     const vits_conv1d_desc& d = g.d[i];
     const size_t wsz = BF ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
     const size_t xsz = (size_t)d.kc * xrs[i];
-    if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) || xsz > (size_t)XTile<BN, BF>::floats)
+    if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) ||
+        xsz > (size_t)XTile<BN, BF, IO16>::floats)
       return VITS_E_UNSUP;
     // 32-bit window offsets
     if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
@@ -634,7 +648,8 @@ int launch_tile(const ConvGroup& g, hipStream_t s) {
     const bool v4 = d.x_tstride == 1 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
                     (d.tin & 3) == 0 && d.pad_left >= 0 &&
                     (reinterpret_cast<uintptr_t>(d.x) & align) == 0 &&
-                    (size_t)d.kc * xrs4[i] <= (size_t)XTile<BN, BF>::floats;
+                    (size_t)d.kc * xrs4[i] <=
+                        (size_t)(d.io16 ? XTile<BN, BF, true>::floats : XTile<BN, BF>::floats);
     nv4 += v4;
     nio += d.io16 != 0;
   }
@@ -681,7 +696,8 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
       bool fits128 = true;
       for (int i = 0; i < g.n; ++i) {
         const int xw_pad128 = (128 + (g.d[i].k - 1) * g.d[i].dil + 3) & ~3;
-        fits128 = fits128 && g.d[i].kc * xw_pad128 <= XTile<128, BF>::floats;
+        fits128 = fits128 && g.d[i].kc * xw_pad128 <= (g.d[i].io16 ? XTile<128, BF, true>::floats
+                                                                    : XTile<128, BF>::floats);
       }
       if (blocks < 512 && fits128) return launch_tile<64, 128, 2, 2, WT>(g, s);
       return launch_tile<64, 256, 1, 4, WT>(g, s);

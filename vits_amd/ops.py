@@ -163,7 +163,8 @@ class PackedConv:
     up_pad: int = 0
     out_channels: int = 0      # channels of the produced tensor
     extra: dict = field(default_factory=dict)
-    wdtype: int = WDT_F32      # WDT_BF16 / WDT_F16: w is [cin_pad/kc][k][kc/8][m_pad][8] 16-bit
+    wdtype: int = WDT_F32      # WDT_BF16 / WDT_F16: w is [cin_pad/16][k][2][m_pad][8] 16-bit
+                               # (16-channel slabs; a K-chunk of kc channels = kc/16 slabs)
 
     @property
     def m_pad(self) -> int:
@@ -171,7 +172,7 @@ class PackedConv:
 
     @property
     def cin_pad(self) -> int:
-        return self.w.shape[0] * self.kc if self.wdtype != WDT_F32 else self.w.shape[0]
+        return self.w.shape[0] * 16 if self.wdtype != WDT_F32 else self.w.shape[0]
 
 
 def _finish_pack(rows_w: torch.Tensor, k: int, tile: int, dil: int = 1) -> tuple[torch.Tensor, int]:

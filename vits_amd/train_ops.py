@@ -39,7 +39,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from ._lib import EPI_STORE, TILE_64x128, TILE_128x128, WDT_BF16, WDT_F16, ConvWgradDesc, check
+from ._lib import (EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128, WDT_BF16,
+                   WDT_F16, ConvWgradDesc, check)
 from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
                   make_desc, make_out, weight_norm_effective)
 
@@ -61,9 +62,33 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
     return _pick_tile_bf16(m, k)
 
 
+# K-chunk of the 16-bit training convs: kc channels (a multiple of 16) with
+# kc * k <= TRAIN_KCK.  A chunk is one barrier-separated step of the
+# kernel's two-stage global->LDS pipeline; at kc = 16 a 1x1 conv has one
+# MFMA k-step per chunk and waits on every chunk's loads.
+TRAIN_KCK = int(os.environ.get("VITS_TRAIN_KCK", "64"))
+_TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32}
+_TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256}
+
+
+def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
+    """Largest kc in (64, 48, 32, 16) that divides cin_pad and fits the
+    kernel's W (kc*k*BM/2 <= 6144 slots) and X staging budgets
+    (conv1d_impl.h XTile: 6144 / 10240 16-bit elements for BN 128 / 256 with
+    16-bit activations, 3072 / 5120 otherwise)."""
+    bm, bn = _TILE_BM[tile], _TILE_BN[tile]
+    xrs = bn + (k - 1) * dil + 8
+    xbudget = (6144 if bn <= 128 else 10240) if io16 else (3072 if bn <= 128 else 5120)
+    for kc in (64, 48, 32):
+        if (kc * k <= TRAIN_KCK and cin_pad % kc == 0 and kc * k * bm // 2 <= 6144
+                and kc * xrs <= xbudget):
+            return kc
+    return 16
+
+
 def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype: int,
             bias: torch.Tensor | None = None, zero: torch.Tensor | None = None,
-            n_out: int | None = None) -> PackedConv:
+            n_out: int | None = None, io16: bool = False) -> PackedConv:
     """16-bit weight image (and, in the same launch, clear ``zero``)."""
     cout, cin, k = w32.shape
     rows, chans = (cin, cout) if transpose else (cout, cin)
@@ -74,12 +99,14 @@ def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype:
         w32.data_ptr(), cout, cin, k, int(transpose), img.data_ptr(), m_pad, cin_pad, wdtype,
         None if zero is None else zero.data_ptr(), 0 if zero is None else zero.numel(),
         _stream_ptr(w32.device)), "vits_conv1d_pack16")
-    return PackedConv(img, bias, chans, rows, k, dil, pad_left, EPI_STORE,
-                      _pick_tile_train(rows, k, n_out), 16, out_channels=rows, wdtype=wdtype)
+    tile = _pick_tile_train(rows, k, n_out)
+    return PackedConv(img, bias, chans, rows, k, dil, pad_left, EPI_STORE, tile,
+                      _train_kc(cin_pad, k, dil, tile, io16), out_channels=rows, wdtype=wdtype)
 
 
 def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
-                 bias: torch.Tensor | None, n_out: int | None = None, n_in: int | None = None):
+                 bias: torch.Tensor | None, n_out: int | None = None, n_in: int | None = None,
+                 io16: bool = False):
     """The forward image and the input-gradient (transposed, tap-reversed)
     image of one weight in ONE launch: (forward PackedConv, backward
     PackedConv)."""
@@ -92,10 +119,11 @@ def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
     check(_lib.load().vits_conv1d_pack16_pair(
         w32.data_ptr(), cout, cin, k, img.data_ptr(), m_pad, cin_pad, img_t.data_ptr(), m_pad_t,
         cin_pad_t, wdtype, _stream_ptr(w32.device)), "vits_conv1d_pack16_pair")
-    fwd = PackedConv(img, bias, cin, cout, k, dil, pad_left, EPI_STORE,
-                     _pick_tile_train(cout, k, n_out), 16, out_channels=cout, wdtype=wdtype)
-    bwd = PackedConv(img_t, None, cout, cin, k, dil, (k - 1) * dil - pad_left, EPI_STORE,
-                     _pick_tile_train(cin, k, n_in), 16, out_channels=cin, wdtype=wdtype)
+    tf, tb = _pick_tile_train(cout, k, n_out), _pick_tile_train(cin, k, n_in)
+    fwd = PackedConv(img, bias, cin, cout, k, dil, pad_left, EPI_STORE, tf,
+                     _train_kc(cin_pad, k, dil, tf, io16), out_channels=cout, wdtype=wdtype)
+    bwd = PackedConv(img_t, None, cout, cin, k, dil, (k - 1) * dil - pad_left, EPI_STORE, tb,
+                     _train_kc(cin_pad_t, k, dil, tb, io16), out_channels=cin, wdtype=wdtype)
     return fwd, bwd
 
 
@@ -304,10 +332,11 @@ class Conv1dHip16(torch.autograd.Function):
         n_out = x.shape[2] + 2 * padding - (k - 1) * dilation
         b32 = None if bias is None else bias.detach().float().contiguous()
         if ctx.needs_input_grad[0]:
-            layer, layer_t = _pack16_pair(w32, dilation, padding, wdtype, b32, n_out, x.shape[2])
+            layer, layer_t = _pack16_pair(w32, dilation, padding, wdtype, b32, n_out, x.shape[2],
+                                          io16=True)
             ctx.layer_t = layer_t
         else:
-            layer = _pack16(w32, False, dilation, padding, wdtype, b32, n_out=n_out)
+            layer = _pack16(w32, False, dilation, padding, wdtype, b32, n_out=n_out, io16=True)
             ctx.layer_t = None
         if res is not None:
             assert res.dtype == x.dtype and res.shape == (x.shape[0], layer.m, n_out)
@@ -331,7 +360,8 @@ class Conv1dHip16(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             layer_t = ctx.layer_t
             if layer_t is None:
-                layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, n_out=x.shape[2])
+                layer_t = _pack16(w32, True, dil, (k - 1) * dil - pad, wdtype, n_out=x.shape[2],
+                                  io16=True)
             ctx.layer_t = None
             dx = _run(dy, layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
                       gmask_slope=slope, io16=True)
