@@ -494,7 +494,9 @@ typedef struct vits_snorm_layer {
   int32_t rows;
   int32_t cols;
   float eps;
-  int32_t reserved;
+  int32_t cl_channels; /* 0: w_sn / dw_sn fp32 like w; C > 0: fp16 channels-  */
+                       /* last [O][kh][kw][C] images of a Conv2d weight       */
+                       /* [O][C][kh][kw] (the autocast MIOpen conv's operand) */
 } vits_snorm_layer;
 int vits_spectral_norm_supported(int rows, int cols);
 int vits_spectral_norm_forward(const vits_snorm_layer* layers, int n, int training, int emu16,

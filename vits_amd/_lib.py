@@ -203,7 +203,7 @@ class SnormLayer(C.Structure):
         ("rows", C.c_int32),
         ("cols", C.c_int32),
         ("eps", C.c_float),
-        ("reserved", C.c_int32),
+        ("cl_channels", C.c_int32),
     ]
 
 

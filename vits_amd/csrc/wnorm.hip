@@ -101,6 +101,19 @@ struct SnGrid {
 };
 constexpr int SN_CHUNK = 4096;  // elements per workgroup in F5 / B1 / B2
 
+// W_sn / dW_sn element of logical index i ([rows][cols] row-major): the same
+// fp32 layout, or (cl_channels = C > 0) an fp16 [O][kh][kw][C] channels-last
+// image of a Conv2d weight [O][C][kh][kw] (cols = C * kh * kw) - what the
+// reference's autocast MIOpen conv gets after casting W / sigma
+__device__ __forceinline__ int64_t sn_cl_index(int64_t i, int cols, int C) {
+  const int64_t o = i / cols;
+  const int rem = (int)(i - o * cols);
+  const int hw = cols / C;
+  const int c = rem / hw;
+  const int p = rem - c * hw;
+  return o * cols + (int64_t)p * C + c;
+}
+
 __device__ __forceinline__ int sn_layer_of(const SnGrid& G, int b) {
   int lo = 0, hi = G.n - 1;
   while (lo < hi) {
@@ -228,7 +241,17 @@ __global__ __launch_bounds__(256) void snorm_out_kernel(const SnGrid G) {
   const int64_t n = (int64_t)T.rows * T.cols;
   const int64_t i0 = (int64_t)(b - G.bstart[l]) * SN_CHUNK;
   for (int64_t i = i0 + threadIdx.x; i < i0 + SN_CHUNK && i < n; i += 256)
-    T.w_sn[i] = T.w[i] / sigma;
+    if (T.cl_channels > 0)
+      reinterpret_cast<_Float16*>(T.w_sn)[sn_cl_index(i, T.cols, T.cl_channels)] =
+          (_Float16)(T.w[i] / sigma);
+    else
+      T.w_sn[i] = T.w[i] / sigma;
+}
+
+__device__ __forceinline__ float sn_dw(const vits_snorm_layer& T, int64_t i) {
+  if (T.cl_channels > 0)
+    return (float)reinterpret_cast<const _Float16*>(T.dw_sn)[sn_cl_index(i, T.cols, T.cl_channels)];
+  return T.dw_sn[i];
 }
 
 // B1: partial[chunk] = sum over the chunk of dW_sn * W
@@ -240,7 +263,7 @@ __global__ __launch_bounds__(256) void snorm_bwd_dot_kernel(const SnGrid G, floa
   const int64_t i0 = (int64_t)(b - G.bstart[l]) * SN_CHUNK;
   __shared__ float red[4];
   float s = 0.f;
-  for (int64_t i = i0 + threadIdx.x; i < i0 + SN_CHUNK && i < n; i += 256) s += T.dw_sn[i] * T.w[i];
+  for (int64_t i = i0 + threadIdx.x; i < i0 + SN_CHUNK && i < n; i += 256) s += sn_dw(T, i) * T.w[i];
   s = block_sum(s, red);
   if (threadIdx.x == 0) part[b] = s;
 }
@@ -264,7 +287,7 @@ __global__ __launch_bounds__(256) void snorm_bwd_kernel(const SnGrid G, const fl
   for (int64_t i = i0 + threadIdx.x; i < i0 + SN_CHUNK && i < n; i += 256) {
     const int r = (int)(i / T.cols);
     const int c = (int)(i - (int64_t)r * T.cols);
-    T.dw[i] = T.dw_sn[i] / sigma + h16(h16(gs * u[r], emu) * h16(v[c], emu), emu);
+    T.dw[i] = sn_dw(T, i) / sigma + h16(h16(gs * u[r], emu) * h16(v[c], emu), emu);
   }
 }
 
@@ -352,6 +375,8 @@ extern "C" int vits_spectral_norm_forward(const vits_snorm_layer* layers, int n,
     const vits_snorm_layer* ls = layers + base;
     for (int i = 0; i < cnt; ++i) {
       VITS_CHECK_ARG(ls[i].w && ls[i].u && ls[i].v && ls[i].w_sn && ls[i].saved);
+      VITS_CHECK_ARG(ls[i].cl_channels >= 0 &&
+                     (ls[i].cl_channels == 0 || ls[i].cols % ls[i].cl_channels == 0));
       if (!vits_spectral_norm_supported(ls[i].rows, ls[i].cols)) return VITS_E_UNSUP;
     }
     SnGrid G;
@@ -395,7 +420,8 @@ extern "C" int vits_spectral_norm_backward(const vits_snorm_layer* layers, int n
     const vits_snorm_layer* ls = layers + base;
     for (int i = 0; i < cnt; ++i)
       VITS_CHECK_ARG(ls[i].w && ls[i].dw_sn && ls[i].dw && ls[i].saved && ls[i].rows > 0 &&
-                     ls[i].cols > 0);
+                     ls[i].cols > 0 && ls[i].cl_channels >= 0 &&
+                     (ls[i].cl_channels == 0 || ls[i].cols % ls[i].cl_channels == 0));
     SnGrid G;
     const int nb = sn_fill(G, ls, cnt, sn_chunks);
     hipLaunchKernelGGL(snorm_bwd_dot_kernel, dim3(nb), dim3(256), 0, s, G, part);

@@ -204,6 +204,12 @@ class GroupedSpectralNorm:
                     self.groups.setdefault(key, []).append(m)
         self.flat = [(m, name, eps) for (_, eps, name), mods in self.groups.items() for m in mods]
         self._fused = None
+        # Conv2d layers the STFT discriminators run on MIOpen (all but the
+        # first, which conv2d_freq lowers onto the HIP conv): their W / sigma
+        # is produced as the fp16 channels-last operand under autocast
+        firsts = {id(sub.convs[0]) for sub in root.modules() if isinstance(sub, STFTDiscriminator)}
+        cl = STFT_D_NHWC and os.environ.get("VITS_SN_CL", "1") != "0"  # A/B switch
+        self.cl16 = [cl and isinstance(m, Conv2d) and id(m) not in firsts for m, _, _ in self.flat]
 
     def _fused_ok(self) -> bool:
         """All layers on the one-launch HIP path (wnorm.spectral_norm_all):
@@ -227,7 +233,8 @@ class GroupedSpectralNorm:
         if self._fused_ok():
             Ws = [getattr(m, n + "_orig") for m, n, _ in self.flat]
             layers = [(getattr(m, n + "_u"), getattr(m, n + "_v"), eps) for m, n, eps in self.flat]
-            for (m, n, _), w in zip(self.flat, wnorm.spectral_norm_all(Ws, layers, training)):
+            outs = wnorm.spectral_norm_all(Ws, layers, training, self.cl16)
+            for (m, n, _), w in zip(self.flat, outs):
                 setattr(m, n, w)
             return
         for (shape, eps, name), mods in self.groups.items():

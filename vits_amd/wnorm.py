@@ -155,7 +155,11 @@ class _SpectralNormAll(torch.autograd.Function):
     @staticmethod
     def forward(ctx, layers, training: bool, emu16: bool, *Ws):
         n = len(Ws)
-        outs = [torch.empty_like(W) for W in Ws]
+        # layers: (u, v, eps, cl) - cl = C > 0: W / sigma as the fp16
+        # channels-last image the autocast MIOpen conv would cast it to
+        outs = [torch.empty(W.shape, device=W.device, dtype=torch.float16,
+                            memory_format=torch.channels_last) if lay[3] else torch.empty_like(W)
+                for W, lay in zip(Ws, layers)]
         shapes = [(W.shape[0], W.numel() // W.shape[0]) for W in Ws]
         offs, tot = [], 0
         for r, c in shapes:
@@ -163,15 +167,17 @@ class _SpectralNormAll(torch.autograd.Function):
             tot += 1 + r + c
         saved = torch.empty(tot, device=Ws[0].device, dtype=torch.float32)
         arr = (SnormLayer * n)()
-        for i, (W, (u, v, eps)) in enumerate(zip(Ws, layers)):
+        for i, (W, (u, v, eps, cl)) in enumerate(zip(Ws, layers)):
             e = arr[i]
             e.w, e.u, e.v, e.w_sn = W.data_ptr(), u.data_ptr(), v.data_ptr(), outs[i].data_ptr()
             e.saved = saved.data_ptr() + 4 * offs[i]
             e.rows, e.cols = shapes[i]
             e.eps = eps
+            e.cl_channels = cl
         check(_lib.load().vits_spectral_norm_forward(arr, n, int(training), int(emu16),
                                                      _stream(saved)), "vits_spectral_norm_forward")
         ctx.offs, ctx.shapes, ctx.emu16 = offs, shapes, emu16
+        ctx.cls = [lay[3] for lay in layers]
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(*Ws, saved)
         return tuple(outs)
@@ -188,13 +194,17 @@ class _SpectralNormAll(torch.autograd.Function):
             arr = (SnormLayer * len(idx))()
             keep = []
             for a, i in enumerate(idx):
-                g = gs[i].contiguous()
+                if ctx.cls[i]:
+                    g = gs[i].to(torch.float16).contiguous(memory_format=torch.channels_last)
+                else:
+                    g = gs[i].float().contiguous()
                 keep.append(g)
                 dWs[i] = torch.empty_like(Ws[i])
                 e = arr[a]
                 e.w, e.dw_sn, e.dw = Ws[i].data_ptr(), g.data_ptr(), dWs[i].data_ptr()
                 e.saved = saved.data_ptr() + 4 * ctx.offs[i]
                 e.rows, e.cols = ctx.shapes[i]
+                e.cl_channels = ctx.cls[i]
             lib = _lib.load()
             nws = lib.vits_spectral_norm_workspace(arr, len(idx))
             ws = torch.empty(max(1, nws), device=saved.device, dtype=torch.float32)
@@ -210,14 +220,19 @@ def spectral_norm_supported(W: torch.Tensor) -> bool:
     return bool(_lib.load().vits_spectral_norm_supported(W.shape[0], W.numel() // W.shape[0]))
 
 
-def spectral_norm_all(Ws, layers, training: bool):
+def spectral_norm_all(Ws, layers, training: bool, cl16=None):
     """W / sigma for every weight (torch.nn.utils.spectral_norm semantics, dim
     0, one power iteration when training); ``layers``: (u, v, eps) per W.
     Inside an fp16 autocast region the reference's fp16 ``mv`` rounding is
-    reproduced."""
+    reproduced, and the 4-D weights flagged in ``cl16`` come out as the fp16
+    channels-last tensors the autocast MIOpen convs consume (the cast and
+    layout copy those convs would make, done in the same kernel)."""
     dev = Ws[0].device.type
     emu16 = torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.float16
-    return _SpectralNormAll.apply(layers, bool(training), bool(emu16), *Ws)
+    cl16 = cl16 or [False] * len(Ws)
+    lay = [(u, v, eps, W.shape[1] if (emu16 and c and W.dim() == 4) else 0)
+           for W, (u, v, eps), c in zip(Ws, layers, cl16)]
+    return _SpectralNormAll.apply(lay, bool(training), bool(emu16), *Ws)
 
 
 def spectral_norm_hook(m: torch.nn.Module, name: str):
