@@ -1,6 +1,6 @@
 import csv, glob, os, sys
 from collections import defaultdict
-base = "gpurun_out/pmc_conv"
+base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_conv"
 for shape in sorted(os.listdir(base)):
     d = os.path.join(base, shape)
     if not os.path.isdir(d):

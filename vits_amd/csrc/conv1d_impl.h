@@ -187,26 +187,48 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
   constexpr int MAXX = XTile<BN, BF, IO16>::regs;
-  constexpr int NU = V4 ? MAXX / 4 : MAXX;  // staging units per thread (blocks or elements)
-  constexpr int UW = V4 ? 4 : 1;            // elements per unit
+  // T4 staging (16-bit activations, V4 rows): a unit is 4 channels x 4 time
+  // steps - four 8-byte row loads, transposed in registers into four 8-byte
+  // [t][4 channels] pieces, one ds_write_b64 each (the element-wise [t][c]
+  // scatter of the other paths costs one ds_write_b16 per element).  Units
+  // of a 16-lane group cover 4 channel quads x 4 time blocks: their LDS
+  // pieces fall on distinct banks for kcp = 4 (mod 16) halves per row.
+  constexpr bool T4 = V4 && IO16;
+  constexpr int NU = T4 ? (XTile<BN, BF, IO16>::floats / 16 + 48 + 255) / 256
+                        : V4 ? MAXX / 4 : MAXX;  // staging units per thread
+  constexpr int UW = V4 ? 4 : 1;            // elements per unit (per row)
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   typedef typename std::conditional<IO16, lpx4, f32x4v>::type x4_t;  // 16-byte / 8-byte unit
-  x4_t xreg4[V4 ? NU : 1];
+  x4_t xreg4[V4 ? NU : 1][T4 ? 4 : 1];
   io_t xreg[V4 ? 1 : NU];
   int xrow[NU];  // window row of unit tid + 256q (1<<24 when it is padding)
   int xoff[NU];  // its global offset relative to row 0 of the chunk
-  const int nunits = V4 ? kc * nb : xsz;
+  int xlds[T4 ? NU : 1];  // T4: the unit's LDS element offset ([t][kcp] image)
+  const int nbq = (nb + 3) >> 2;
+  const int nunits = T4 ? kc * nbq : V4 ? kc * nb : xsz;
 #pragma unroll
   for (int q = 0; q < NU; ++q) {
     const int u = tid + q * 256;
-    const int per = V4 ? nb : xw_pad;
-    const int r = u / per;
-    const int c = u - r * per;
-    const int t = c * UW;  // first window column of the unit
-    const int tt = xstart + t;
-    const bool ok = u < nunits && (V4 || t < xw) && tt >= 0 && tt < p.tin;
-    xrow[q] = ok ? r : (1 << 24);
-    xoff[q] = ok ? r * p.x_cstride + tt * (int)xts : 0;
+    if constexpr (T4) {
+      const int lo = u & 15, hi = u >> 4;
+      const int hq = hi / nbq;
+      const int cq = (lo & 3) + 4 * hq;                  // channel quad
+      const int tb = (lo >> 2) + 4 * (hi - hq * nbq);    // 4-step time block
+      const int tt = xstart + 4 * tb;
+      const bool ok = u < nunits && tb < nb && tt >= 0 && tt < p.tin;
+      xrow[q] = ok ? 4 * cq : (1 << 24);
+      xoff[q] = ok ? 4 * cq * p.x_cstride + tt : 0;
+      xlds[q] = (u < nunits && tb < nb) ? 4 * tb * kcp + 4 * cq : -1;
+    } else {
+      const int per = V4 ? nb : xw_pad;
+      const int r = u / per;
+      const int c = u - r * per;
+      const int t = c * UW;  // first window column of the unit
+      const int tt = xstart + t;
+      const bool ok = u < nunits && (V4 || t < xw) && tt >= 0 && tt < p.tin;
+      xrow[q] = ok ? r : (1 << 24);
+      xoff[q] = ok ? r * p.x_cstride + tt * (int)xts : 0;
+    }
   }
 
   // ---- W chunk: LDS-DMA, one 1 KiB piece (256 floats) per wave instruction;
@@ -250,12 +272,21 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
 #pragma unroll
     for (int q = 0; q < NU; ++q) {
       if (q * 256 < nunits) {  // workgroup-uniform: no exec-mask branch
-        const bool ok = xrow[q] < lim;
-        const io_t* src = ok ? base + xoff[q] : xb;
-        if constexpr (V4)
-          xreg4[q] = *reinterpret_cast<const x4_t*>(src);
-        else
-          xreg[q] = *src;
+        if constexpr (T4) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool ok = xrow[q] + i < lim;
+            const io_t* src = ok ? base + xoff[q] + i * p.x_cstride : xb;
+            xreg4[q][i] = *reinterpret_cast<const x4_t*>(src);
+          }
+        } else {
+          const bool ok = xrow[q] < lim;
+          const io_t* src = ok ? base + xoff[q] : xb;
+          if constexpr (V4)
+            xreg4[q][0] = *reinterpret_cast<const x4_t*>(src);
+          else
+            xreg[q] = *src;
+        }
       }
     }
   };
@@ -268,12 +299,39 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
       if (q * 256 < nunits) {
         const int u = tid + q * 256;
         const bool ok = xrow[q] < lim;
-        if (u < nunits) {
+        if constexpr (T4) {
+          if (xlds[q] >= 0) {
+            // rows i of the unit -> 4 time steps of 4 channels; padding rows
+            // / blocks are zero, the leaky-relu prologue runs in fp32 (the
+            // reference's autocast leaky_relu rounds once, from fp32)
+            lpx4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const bool oki = xrow[q] + i < lim;
+              if (act_in) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  float t = (float)xreg4[q][i][e];
+                  t = t < 0.f ? t * slope : t;
+                  v[i][e] = (lp_t)(oki ? t : 0.f);
+                }
+              } else {
+                v[i] = oki ? xreg4[q][i] : lpx4{};
+              }
+            }
+            lp_t* xh = reinterpret_cast<lp_t*>(xs) + xlds[q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const lpx4 w = {v[0][e], v[1][e], v[2][e], v[3][e]};
+              *reinterpret_cast<lpx4*>(xh + e * kcp) = w;
+            }
+          }
+        } else if (u < nunits) {
           if constexpr (V4) {
             f32x4v v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float t = (float)xreg4[q][e];
+              float t = (float)xreg4[q][0][e];
               if (act_in) t = t < 0.f ? t * slope : t;
               v[e] = ok ? t : 0.f;
             }
@@ -598,6 +656,11 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     // 32-bit window offsets
     if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
       return VITS_E_UNSUP;
+    if (V4 && IO16) {  // T4 staging: kc/4 channel quads x ceil(nb/4)*4 blocks
+      constexpr int nu = (XTile<BN, BF, IO16>::floats / 16 + 48 + 255) / 256;
+      if (d.kc % 16 || (size_t)d.kc * ((xrs[i] / 4 + 3) / 4) > (size_t)nu * 256)
+        return VITS_E_UNSUP;
+    }
     const size_t xslots = BF ? (xrs[i] * (d.kc + 4) + 1) / 2 : xsz;
     // + tail pad: the software pipeline reads one k-step past the last chunk
     const size_t l = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xrs[i] + 64);
