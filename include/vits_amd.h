@@ -123,7 +123,11 @@ typedef struct vits_conv1d_desc {
   /* VITS_WDT_BF16 / VITS_WDT_F16 (w = 16-bit [cin_pad/kc][k][kc/8][m_pad]  */
   /* [8], kc % 16 == 0; activations stay fp32 in HBM and are rounded to the */
   /* 16-bit type when staged; fp32 accumulation:                           */
-  /* v_mfma_f32_32x32x16_bf16 / _f16)                                       */
+  /* v_mfma_f32_32x32x16_bf16 / _f16), or VITS_WDT_F32S (w = the fp32     */
+  /* [cin_pad/16][k][2][m_pad][8] slab image, kc % 16 == 0: fp32 operands  */
+  /* split exactly into three bf16 terms in registers, six bf16 MFMAs per  */
+  /* 16-deep k-step (hi*hi, hi*mid, mid*hi, mid*mid, hi*lo, lo*hi), fp32   */
+  /* accumulation; error vs fp64 at the exact-fp32 kernel's level)         */
   int32_t wdtype;
   /* single-output STORE only (the input gradient of a conv whose forward   */
   /* fused a leaky-relu prologue): v *= gmask[b][row][n] > 0 ? 1 : slope    */
@@ -142,6 +146,7 @@ typedef struct vits_conv1d_desc {
 #define VITS_WDT_F32 0
 #define VITS_WDT_BF16 1
 #define VITS_WDT_F16 2
+#define VITS_WDT_F32S 3
 
 int vits_conv1d_forward(const vits_conv1d_desc* d, int batch, void* stream);
 

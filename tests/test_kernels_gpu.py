@@ -29,7 +29,8 @@ def _close(a, b, tol=RTOL, what=""):
     (2, 64, 64, 7, 3, 1000), (2, 16, 32, 11, 1, 777), (1, 513, 256, 1, 1, 64),
     (2, 256, 96, 1, 1, 130), (1, 96, 256, 1, 1, 33), (2, 32, 32, 3, 5, 2000),
 ])
-def test_conv1d_store(device, B, cin, cout, k, dil, T):
+@pytest.mark.parametrize("wdt", [ops.WDT_F32, ops.WDT_F32S])
+def test_conv1d_store(device, B, cin, cout, k, dil, T, wdt):
     g = torch.Generator().manual_seed(B * 1000 + cin + k)
     x = torch.randn(B, cin, T, generator=g)
     w = torch.randn(cout, cin, k, generator=g) / (cin * k) ** 0.5
@@ -38,13 +39,15 @@ def test_conv1d_store(device, B, cin, cout, k, dil, T):
     ref = F.conv1d(F.leaky_relu(x, 0.1), w, b, padding=pad, dilation=dil)
     res = torch.randn(B, cout, T, generator=g)
     ref = ref + res
-    layer = ops.pack_conv(w.to(device), b.to(device), dilation=dil)
+    with ops.pack_lowp(wdt):
+        layer = ops.pack_conv(w.to(device), b.to(device), dilation=dil)
     out = ops.conv1d(x.to(device), layer, in_slope=0.1, residual=res.to(device))
     _close(out, ref, what="conv1d")
 
 
 @pytest.mark.parametrize("B,C,k,dil,T", [(2, 256, 3, 1, 200), (1, 32, 11, 5, 900), (2, 128, 7, 3, 333)])
-def test_conv1d_gate_cond(device, B, C, k, dil, T):
+@pytest.mark.parametrize("wdt", [ops.WDT_F32, ops.WDT_F32S])
+def test_conv1d_gate_cond(device, B, C, k, dil, T, wdt):
     g = torch.Generator().manual_seed(7 + C)
     x = torch.randn(B, C, T, generator=g)
     w = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
@@ -55,23 +58,51 @@ def test_conv1d_gate_cond(device, B, C, k, dil, T):
     xa, xb = xt.chunk(2, 1)
     sa, sb = cond.chunk(2, 1)
     ref = torch.tanh(xa + sa.unsqueeze(-1)) * torch.sigmoid(xb + sb.unsqueeze(-1))
-    layer = ops.pack_conv(w.to(device), b.to(device), dilation=dil, gate=True)
+    with ops.pack_lowp(wdt):
+        layer = ops.pack_conv(w.to(device), b.to(device), dilation=dil, gate=True)
     out = ops.conv1d(x.to(device), layer, in_slope=0.1, cond=cond.to(device))
     _close(out, ref, what="gate")
 
 
 @pytest.mark.parametrize("B,cin,cout,K,u,T", [(1, 512, 256, 16, 8, 40), (2, 256, 128, 12, 6, 37),
                                              (2, 128, 64, 4, 2, 301), (1, 64, 32, 4, 2, 1000)])
-def test_conv_transpose_polyphase(device, B, cin, cout, K, u, T):
+@pytest.mark.parametrize("wdt", [ops.WDT_F32, ops.WDT_F32S])
+def test_conv_transpose_polyphase(device, B, cin, cout, K, u, T, wdt):
     g = torch.Generator().manual_seed(K + cin)
     x = torch.randn(B, cin, T, generator=g)
     w = torch.randn(cin, cout, K, generator=g) / (cin * 2) ** 0.5
     b = torch.randn(cout, generator=g) * 0.1
     pad = (K - u) // 2
     ref = F.conv_transpose1d(F.leaky_relu(x, 0.1), w, b, stride=u, padding=pad)
-    layer = ops.pack_conv_transpose(w.to(device), b.to(device), u, pad)
+    with ops.pack_lowp(wdt):
+        layer = ops.pack_conv_transpose(w.to(device), b.to(device), u, pad)
     out = ops.conv1d(x.to(device), layer, in_slope=0.1)
     _close(out, ref, what="convT")
+
+
+@pytest.mark.parametrize("C,k,dil,T", [(256, 3, 1, 1024), (128, 7, 3, 999), (256, 11, 5, 640),
+                                       (512, 5, 1, 200)])
+def test_conv1d_split_f32_matches_exact_f32_error(device, C, k, dil, T):
+    """Split fp32 (VITS_WDT_F32S: three exact bf16 terms, six bf16 MFMAs)
+    against an fp64 convolution: its rms / max error must stay at the level
+    of the exact-fp32 kernel's (v_mfma_f32_32x32x2_f32) - within 1.5x - on
+    the decoder's shapes.  Measured on MI355X: split 2.9e-7..8.4e-7 rms vs
+    exact 3.4e-7..9.5e-7 (tools/split_accuracy.py)."""
+    g = torch.Generator().manual_seed(C + k)
+    x = torch.randn(2, C, T, generator=g, dtype=torch.float64)
+    w = torch.randn(C, C, k, generator=g, dtype=torch.float64) / (C * k) ** 0.5
+    ref = F.conv1d(x, w, padding=(k - 1) * dil // 2, dilation=dil)
+    rms = ref.pow(2).mean().sqrt().item()
+    errs = {}
+    for wdt in (ops.WDT_F32, ops.WDT_F32S):
+        with ops.pack_lowp(wdt):
+            layer = ops.pack_conv(w.float().to(device), None, dilation=dil)
+        assert layer.wdtype == wdt
+        out = ops.conv1d(x.float().to(device), layer).double().cpu()
+        e = out - ref
+        errs[wdt] = (e.pow(2).mean().sqrt().item() / rms, e.abs().max().item() / rms)
+    assert errs[ops.WDT_F32S][0] <= 1.5 * errs[ops.WDT_F32][0], errs
+    assert errs[ops.WDT_F32S][1] <= 1.5 * errs[ops.WDT_F32][1], errs
 
 
 def test_conv1d_masked_split_accumulate(device):

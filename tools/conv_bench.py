@@ -23,6 +23,8 @@ shapes.append(("pre", 192, 512, 7, 1, Ty, False, None))
 
 only = os.environ.get("ONLY")
 BF = os.environ.get("BF", "0") == "1"
+WDT = int(os.environ.get("WDT", "1" if BF else "0"))  # 0 f32, 1 bf16, 3 split-f32
+CHECK = os.environ.get("CHECK", "0") == "1"  # error vs the exact-f32 kernel and fp64
 tiles = [int(t) for t in os.environ.get("TILES", "").split(",") if t]
 kcms = [int(t) for t in os.environ.get("KCM", "1").split(",") if t]
 reps = int(os.environ.get("REPS", "5"))
@@ -35,14 +37,14 @@ for name, cin, cout, k, d, T, gate, up in shapes:
     if up:
         u, K = up
         w = torch.randn(cin, cout, K, device=dev) * 0.05
-        with ops.pack_bf16(BF):
+        with ops.pack_lowp(WDT):
             layer = ops.pack_conv_transpose(w, torch.zeros(cout, device=dev), u, (K - u) // 2)
         y = torch.empty(B, cout, T * u, device=dev)
         desc = make_desc(layer, x, make_out(y), in_slope=0.1, t_out=T * u)
         flops = 2 * B * cout * T * u * cin * (K // u)
     else:
         w = torch.randn(cout, cin, k, device=dev) * 0.05
-        with ops.pack_bf16(BF):
+        with ops.pack_lowp(WDT):
             layer = ops.pack_conv(w, torch.zeros(cout, device=dev), dilation=d, gate=gate)
         y = torch.empty(B, layer.out_channels, T, device=dev)
         res_t = None if gate else torch.randn(B, cout, T, device=dev)

@@ -84,6 +84,8 @@ struct XTile {
 };
 // bf16 W stage budget in float slots (2 bf16 each): k=11, kc=16, BM=64 fits
 constexpr int VITS_W_TILE_BF = 6144;
+// split-fp32 (VITS_WDT_F32S) W stage in floats: k=11, kc=16, BM=64 fits
+constexpr int VITS_W_TILE_SPL = 11264;
 // low-precision element type of weight type WT (VITS_WDT_BF16 / VITS_WDT_F16)
 template <int WT>
 struct LowP {
@@ -94,6 +96,32 @@ struct LowP<VITS_WDT_F16> {
   typedef _Float16 T;
 };
 typedef __attribute__((address_space(3))) void* lds_void_t;
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x8_t __attribute__((ext_vector_type(8)));
+// Exact three-term split of fp32 values into bf16: h = x truncated to bf16,
+// m = (x - h) truncated, l = x - h - m (<= 8 significant bits, so exact in
+// bf16).  Both subtractions are exact (they clear leading significand bits),
+// hence x == h + m + l bit for bit.  Products of two terms have <= 16
+// significant bits and are exact in the MFMA's fp32 products; the six terms
+// kept (hh, hm, mh, mm, hl, lh) drop m*l' + l*m' + l*l' < 2^-22 |x||w|, the
+// order of one fp32 rounding of the product.
+__device__ __forceinline__ void split3_bf16(const f32x8_t& x, bf16x8_t& h, bf16x8_t& m,
+                                            bf16x8_t& l) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    // (the element is copied out first: __builtin_bit_cast of an ext-vector
+    // element expression reads element 0 on this compiler)
+    const float xe = x[e];
+    const float hf = __uint_as_float(__float_as_uint(xe) & 0xffff0000u);
+    const float r = xe - hf;
+    const float mf = __uint_as_float(__float_as_uint(r) & 0xffff0000u);
+    // hf, mf are bf16 values already: the conversions are exact
+    h[e] = (__bf16)hf;
+    m[e] = (__bf16)mf;
+    l[e] = (__bf16)(r - mf);
+  }
+}
 
 __device__ __forceinline__ float fast_sigmoid(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
@@ -121,16 +149,21 @@ struct ConvGroup {
 // activations in fp16, as the reference's autocast convs return them),
 // half the bytes of the fp32-I/O kernel; accumulation stays fp32.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false>
-__global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) {
+__global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
   static_assert(!IO16 || WT != VITS_WDT_F32, "IO16 needs a 16-bit operand type");
   const int gi = (int)blockIdx.z / G.batch;
   const vits_conv1d_desc& p = G.d[gi];
   if ((int)blockIdx.x * BN >= p.n_out || (int)blockIdx.y * BM >= p.m) return;
-  constexpr bool BF = WT != VITS_WDT_F32;  // 16-bit operands (bf16 or fp16)
+  constexpr bool BF = WT != VITS_WDT_F32;  // 16-channel slab layout, 16-deep k-steps
+  // split fp32: the slab layouts hold fp32 (LDS and W image), split into
+  // three bf16 terms in registers per fragment (split3_bf16)
+  constexpr bool SPL = WT == VITS_WDT_F32S;
+  constexpr int WQ = SPL ? 8 : 4;  // float slots per (W row, 8 channels)
   typedef typename LowP<WT>::T lp_t;
   typedef lp_t lpx8 __attribute__((ext_vector_type(8)));
   typedef lp_t lpx4 __attribute__((ext_vector_type(4)));
   typedef typename std::conditional<IO16, lp_t, float>::type io_t;  // x / res / y element
+  typedef typename std::conditional<SPL, float, lp_t>::type xe_t;   // slab-layout LDS element
   constexpr int WM = BM / WAVES_M;
   constexpr int WN = BN / WAVES_N;
   constexpr int TM = WM / 32;
@@ -145,7 +178,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   const int xw = BN + (k - 1) * dil;
   const int xw_pad = (xw + 3) & ~3;
   const int wrows = kc * k;
-  const int wsz = BF ? wrows * BM / 2 : wrows * BM;  // W stage in float slots
+  const int wsz = (BF && !SPL) ? wrows * BM / 2 : wrows * BM;  // W stage in float slots
   // X window geometry.  Scalar staging (any strides): rows of xw_pad
   // elements starting at column xstart.  V4 staging (time-contiguous rows,
   // 16-byte aligned, tin % 4 == 0): 16-byte blocks from the aligned column
@@ -157,7 +190,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
   // bf16 path: the window sits in LDS as bf16 [t][kc + 4] (channel-contiguous
   // per time step, 8-byte aligned rows) so a B fragment is two ds_read_b64
   const int kcp = kc + 4;
-  const int xslots = BF ? (xrs * kcp + 1) / 2 : xsz;  // LDS float slots
+  const int xslots = BF ? (SPL ? xrs * kcp : (xrs * kcp + 1) / 2) : xsz;  // LDS float slots
   // two stages: [W0][X0][W1][X1]
   float* const stage0 = smem;
   float* const stage1 = smem + wsz + xslots;
@@ -240,10 +273,10 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
     //   the packed image is [cin_pad/16][k][2][m_pad][8] (16-channel slabs)
     //   and a chunk of kc = 16 s channels is s slabs: LDS row (j, c8) of the
     //   [k][kc/8][BM][8] chunk image comes from slab c8/2, tap j, half c8&1
-    const int L = BF ? BM * 4 : BM;
-    const float* wsrc = BF ? p.w + ((int64_t)(c0 / 16) * k * 2 * p.m_pad + m0) * 4
+    const int L = BF ? BM * WQ : BM;
+    const float* wsrc = BF ? p.w + ((int64_t)(c0 / 16) * k * 2 * p.m_pad + m0) * WQ
                            : p.w + (int64_t)c0 * k * p.m_pad + m0;
-    const int64_t S = BF ? (int64_t)p.m_pad * 4 : p.m_pad;
+    const int64_t S = BF ? (int64_t)p.m_pad * WQ : p.m_pad;
     const int c8n = kc >> 3;
     const int pieces = (wsz + 255) >> 8;
     for (int q = wid; q < pieces; q += 4) {
@@ -338,9 +371,9 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
             const int r = u / nb;
             const int c = u - r * nb;
             if constexpr (BF) {
-              lp_t* xh = reinterpret_cast<lp_t*>(xs);
+              xe_t* xh = reinterpret_cast<xe_t*>(xs);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) xh[(4 * c + e) * kcp + r] = (lp_t)v[e];
+              for (int e = 0; e < 4; ++e) xh[(4 * c + e) * kcp + r] = (xe_t)v[e];
             } else {
               *reinterpret_cast<f32x4v*>(xs + r * xrs + 4 * c) = v;
             }
@@ -351,7 +384,7 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
             if constexpr (BF) {
               const int r = u / xw_pad;
               const int t = u - r * xw_pad;
-              reinterpret_cast<lp_t*>(xs)[t * kcp + r] = (lp_t)v;
+              reinterpret_cast<xe_t*>(xs)[t * kcp + r] = (xe_t)v;
             } else {
               xs[u] = v;
             }
@@ -381,7 +414,64 @@ __global__ __launch_bounds__(256, 3) void conv1d_mfma_kernel(const ConvGroup G) 
 
     const float* ws = cur;
     const float* xs = cur + wsz;
-    if constexpr (BF) {
+    if constexpr (SPL) {
+      // k-step = (tap j, 16 channels) as in the 16-bit path below, on fp32
+      // slabs: A = two 16-byte reads of W image [j][c8][row][8], B = two of
+      // the [t][kcp] window; each fragment split into three bf16 terms, six
+      // MFMAs per (mi, ni)
+      const char* wbytes = reinterpret_cast<const char*>(ws);
+      const int c8n = kc >> 3;
+      const int G = kc >> 4;
+      const int nsteps = k * G;
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      auto load = [&](int st, f32x8_t* a, f32x8_t* bb) {
+        const int j = st / G;
+        const int g = st - j * G;
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          const f4* ap = reinterpret_cast<const f4*>(
+              wbytes + ((int64_t)((j * c8n + 2 * g + lhi) * BM + wm + mi * 32 + l32) << 5));
+          a[mi] = __builtin_shufflevector(ap[0], ap[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+          const f4* xp = reinterpret_cast<const f4*>(
+              xs + (wn + ni * 32 + l32 + j * dil + xsh) * kcp + 16 * g + 8 * lhi);
+          bb[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      };
+      auto mma = [&](const f32x8_t* a, const f32x8_t* bb) {
+        bf16x8_t ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) split3_bf16(a[mi], ah[mi], am[mi], al[mi]);
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) split3_bf16(bb[ni], bh[ni], bm[ni], bl[ni]);
+        // small terms first
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) {
+            f32x16 c = acc[mi][ni];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bl[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mi], bh[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mi], bm[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bm[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mi], bh[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bh[ni], c, 0, 0, 0);
+            acc[mi][ni] = c;
+          }
+      };
+      f32x8_t a0[TM], b0[TN], a1[TM], b1[TN];
+      load(0, a0, b0);
+      int st = 0;
+      for (; st + 2 <= nsteps; st += 2) {
+        load(st + 1, a1, b1);
+        mma(a0, b0);
+        load(st + 2, a0, b0);
+        mma(a1, b1);
+      }
+      if (st < nsteps) mma(a0, b0);
+    } else if constexpr (BF) {
       // k-step = (tap j, 16 channels): A = one 16-byte bf16x8 read per
       // 32-row fragment (W image [j][c8][row][8]); B = 8 channel rows of the
       // fp32 X window at column n + j*dil, rounded to bf16 in registers
@@ -648,9 +738,10 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
   int gx = 0, gy = 0;
   for (int i = 0; i < g.n; ++i) {
     const vits_conv1d_desc& d = g.d[i];
-    const size_t wsz = BF ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
+    constexpr bool SPL = WT == VITS_WDT_F32S;
+    const size_t wsz = (BF && !SPL) ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
     const size_t xsz = (size_t)d.kc * xrs[i];
-    if (wsz > (size_t)(BF ? VITS_W_TILE_BF : VITS_W_TILE) ||
+    if (wsz > (size_t)(SPL ? VITS_W_TILE_SPL : BF ? VITS_W_TILE_BF : VITS_W_TILE) ||
         xsz > (size_t)XTile<BN, BF, IO16>::floats)
       return VITS_E_UNSUP;
     // 32-bit window offsets
@@ -661,7 +752,7 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
       if (d.kc % 16 || (size_t)d.kc * ((xrs[i] / 4 + 3) / 4) > (size_t)nu * 256)
         return VITS_E_UNSUP;
     }
-    const size_t xslots = BF ? (xrs[i] * (d.kc + 4) + 1) / 2 : xsz;
+    const size_t xslots = BF ? (SPL ? xrs[i] * (d.kc + 4) : (xrs[i] * (d.kc + 4) + 1) / 2) : xsz;
     // + tail pad: the software pipeline reads one k-step past the last chunk
     const size_t l = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xrs[i] + 64);
     if (l > lds) lds = l;
@@ -669,6 +760,7 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     if (x > gx) gx = x;
     if (y > gy) gy = y;
   }
+  if (lds > 160 * 1024) return VITS_E_UNSUP;
   dim3 grid(gx, gy, g.n * g.batch);
   dim3 block(256);
   const vits_conv1d_desc& d = g.d[0];
@@ -778,3 +870,4 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
 int vits_conv1d_dispatch_f32(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_bf16(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_f16(const vits_conv::ConvGroup& g, hipStream_t s);
+int vits_conv1d_dispatch_f32s(const vits_conv::ConvGroup& g, hipStream_t s);

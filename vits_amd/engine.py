@@ -48,6 +48,16 @@ def _param_signature(module: torch.nn.Module):
     return (first, ver, n)
 
 
+# How fp32 models run their convs: "split" (default) = fp32 operands split
+# exactly into three bf16 terms on the bf16 MFMA (VITS_WDT_F32S, fp32-level
+# error, see csrc/conv1d_impl.h split3_bf16), "exact" = the f32-input MFMA
+# (v_mfma_f32_32x32x2_f32, bitwise an fp32 fma chain).
+FP32_MODE = os.environ.get("VITS_FP32_MODE", "split")
+if FP32_MODE not in ("split", "exact"):
+    raise ValueError(f"VITS_FP32_MODE={FP32_MODE!r}: expected 'split' or 'exact'")
+FP32_WDTYPE = ops.WDT_F32S if FP32_MODE == "split" else ops.WDT_F32
+
+
 def get_plan(module: torch.nn.Module, builder):
     sig = _param_signature(module)
     plan = module.__dict__.get(_PLAN_ATTR)
@@ -57,7 +67,7 @@ def get_plan(module: torch.nn.Module, builder):
         # its own type (fp32 activations, fp32 accumulation); fp32 models run
         # exact fp32
         dt = sig[0][2] if sig[0] is not None else torch.float32
-        wdt = {torch.bfloat16: ops.WDT_BF16, torch.float16: ops.WDT_F16}.get(dt, ops.WDT_F32)
+        wdt = {torch.bfloat16: ops.WDT_BF16, torch.float16: ops.WDT_F16}.get(dt, FP32_WDTYPE)
         with torch.no_grad(), ops.pack_lowp(wdt):
             plan = builder(module)
         plan.signature = sig

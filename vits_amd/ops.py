@@ -17,7 +17,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
+from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, WDT_F32S, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
                    ResblockPairDesc,
                    EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS,
                    check)
@@ -211,13 +211,49 @@ def pack_bf16(enabled: bool = True):
     return pack_lowp(WDT_BF16 if enabled else WDT_F32)
 
 
+def _pick_tile_f32s(m: int, k: int) -> int:
+    """Split-fp32 tile (VITS_WDT_F32S), from the per-shape sweep of
+    tools/conv_bench.py (WDT=3 TILES=0,1,2,3) on MI355X at B=16, Ty=500:
+    k <= 3 -> 128x128 (256/128-channel stages 126-136 TF/s vs 102-124 for
+    64x256), k = 6..8 -> 32x256 (131-135 vs 120-130), otherwise 64x256
+    (k=11: 138-144; flow k=5: 114)."""
+    if k <= 3 and m >= 128:
+        return TILE_128x128
+    if 6 <= k <= 8:
+        return TILE_32x256
+    return TILE_64x256
+
+
+# Split-fp32 layers need >= this many GEMM rows: the sweep above measured it
+# ahead of the exact-f32 kernel on every 128- / 256-channel decoder conv
+# (+8..35 %), the upsamplers, conv_pre and the flow, but behind it on the
+# 32-channel stage (k=3 65 vs 75, k=11 80 vs 108 TF/s); the 32- / 64-channel
+# stages keep exact fp32 and the fused ResBlock2-pair kernel.
+F32S_MIN_ROWS = 128
+
+
 def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
     """Re-pack an fp32 layer for the 16-bit-MFMA kernel variant (bf16 or
     fp16 operands, fp32 accumulation): K-chunks of 16 channels, W as
     [cin_pad/16][k][2][m_pad][8] (one 16-byte A fragment per row and 8
-    channels), tile by _pick_tile_bf16."""
+    channels), tile by _pick_tile_bf16.  WDT_F32S keeps that slab image in
+    fp32 (split into three exact bf16 terms inside the kernel)."""
     if layer.wdtype != WDT_F32 or wdtype == WDT_F32:
         return layer
+    if wdtype == WDT_F32S:
+        if layer.m < F32S_MIN_ROWS:
+            return layer
+        kc = 16
+        w32 = layer.w[:layer.cin]
+        cin_pad = (layer.cin + kc - 1) // kc * kc
+        k, m_pad = w32.shape[1], w32.shape[2]
+        w = w32.new_zeros(cin_pad, k, m_pad)
+        w[:layer.cin] = w32
+        w = w.view(cin_pad // kc, kc // 8, 8, k, m_pad).permute(0, 3, 1, 4, 2).contiguous()
+        return PackedConv(w, layer.bias, layer.cin, layer.m, layer.k, layer.dil,
+                          layer.pad_left, layer.epi, _pick_tile_f32s(layer.m, layer.k), kc,
+                          up_u=layer.up_u, up_pad=layer.up_pad,
+                          out_channels=layer.out_channels, extra=layer.extra, wdtype=wdtype)
     kc = 16
     w32 = layer.w[:layer.cin]                          # [cin, k, m_pad]
     cin_pad = (layer.cin + kc - 1) // kc * kc
