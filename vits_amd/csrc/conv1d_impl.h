@@ -123,6 +123,21 @@ __device__ __forceinline__ void split3_bf16(const f32x8_t& x, bf16x8_t& h, bf16x
   }
 }
 
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split3_bf16x4(const float __attribute__((ext_vector_type(4)))& x,
+                                              bf16x4_t& h, bf16x4_t& m, bf16x4_t& l) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float xe = x[e];
+    const float hf = __uint_as_float(__float_as_uint(xe) & 0xffff0000u);
+    const float r = xe - hf;
+    const float mf = __uint_as_float(__float_as_uint(r) & 0xffff0000u);
+    h[e] = (__bf16)hf;
+    m[e] = (__bf16)mf;
+    l[e] = (__bf16)(r - mf);
+  }
+}
+
 __device__ __forceinline__ float fast_sigmoid(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
@@ -190,10 +205,18 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   // bf16 path: the window sits in LDS as bf16 [t][kc + 4] (channel-contiguous
   // per time step, 8-byte aligned rows) so a B fragment is two ds_read_b64
   const int kcp = kc + 4;
-  const int xslots = BF ? (SPL ? xrs * kcp : (xrs * kcp + 1) / 2) : xsz;  // LDS float slots
-  // two stages: [W0][X0][W1][X1]
+  // split fp32: the window is staged pre-split, three bf16 planes [t][kcp]
+  // (hi, mid, lo) of xpl elements each, in ONE buffer [W0][W1][X] (the W
+  // chunks stay double-buffered; the X chunk is written between two
+  // barriers) - the planes cost 1.5x the fp32 bytes, a second X stage would
+  // halve the workgroups per CU
+  const int xpl = xrs * kcp;
+  const int xslots = BF ? (SPL ? (3 * xpl + 1) / 2 : (xpl + 1) / 2) : xsz;  // LDS float slots
+  // two stages: [W0][X0][W1][X1] (split fp32: [W0][W1][X])
   float* const stage0 = smem;
-  float* const stage1 = smem + wsz + xslots;
+  float* const stage1 = SPL ? smem + wsz : smem + wsz + xslots;
+  float* const xbuf1 = SPL ? smem + 2 * wsz : stage0 + wsz;  // X of stage 0
+  float* const xbuf2 = SPL ? xbuf1 : stage1 + wsz;            // X of stage 1
 
   const int b = (int)blockIdx.z - gi * G.batch;
   const int n0 = blockIdx.x * BN;
@@ -226,12 +249,13 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   // scatter of the other paths costs one ds_write_b16 per element).  Units
   // of a 16-lane group cover 4 channel quads x 4 time blocks: their LDS
   // pieces fall on distinct banks for kcp = 4 (mod 16) halves per row.
-  constexpr bool T4 = V4 && IO16;
+  constexpr bool T4 = V4 && (IO16 || SPL);
   constexpr int NU = T4 ? (XTile<BN, BF, IO16>::floats / 16 + 48 + 255) / 256
                         : V4 ? MAXX / 4 : MAXX;  // staging units per thread
   constexpr int UW = V4 ? 4 : 1;            // elements per unit (per row)
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   typedef typename std::conditional<IO16, lpx4, f32x4v>::type x4_t;  // 16-byte / 8-byte unit
+  typedef typename std::conditional<SPL, f32x4v, lpx4>::type xe4_t;  // T4 LDS piece
   x4_t xreg4[V4 ? NU : 1][T4 ? 4 : 1];
   io_t xreg[V4 ? 1 : NU];
   int xrow[NU];  // window row of unit tid + 256q (1<<24 when it is padding)
@@ -324,20 +348,43 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
     }
   };
   // ---- registers -> LDS stage (zero padding + leaky-relu prologue) -----------
-  auto lstore = [&](float* st, int c0) {
-    float* xs = st + wsz;
+  auto lstore = [&](float* xs, int c0) {
     const int lim = p.cin - c0;
 #pragma unroll
     for (int q = 0; q < NU; ++q) {
       if (q * 256 < nunits) {
         const int u = tid + q * 256;
         const bool ok = xrow[q] < lim;
-        if constexpr (T4) {
+        if constexpr (T4 && SPL) {
+          if (xlds[q] >= 0) {
+            f32x4v v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const bool oki = xrow[q] + i < lim;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float t = xreg4[q][i][e];
+                if (act_in) t = t < 0.f ? t * slope : t;
+                v[i][e] = oki ? t : 0.f;
+              }
+            }
+            __bf16* xh = reinterpret_cast<__bf16*>(xs) + xlds[q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const f32x4v w = {v[0][e], v[1][e], v[2][e], v[3][e]};
+              lpx4 h4, m4, l4;
+              split3_bf16x4(w, h4, m4, l4);
+              *reinterpret_cast<lpx4*>(xh + e * kcp) = h4;
+              *reinterpret_cast<lpx4*>(xh + xpl + e * kcp) = m4;
+              *reinterpret_cast<lpx4*>(xh + 2 * xpl + e * kcp) = l4;
+            }
+          }
+        } else if constexpr (T4) {
           if (xlds[q] >= 0) {
             // rows i of the unit -> 4 time steps of 4 channels; padding rows
             // / blocks are zero, the leaky-relu prologue runs in fp32 (the
             // reference's autocast leaky_relu rounds once, from fp32)
-            lpx4 v[4];
+            xe4_t v[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const bool oki = xrow[q] + i < lim;
@@ -346,17 +393,17 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
                 for (int e = 0; e < 4; ++e) {
                   float t = (float)xreg4[q][i][e];
                   t = t < 0.f ? t * slope : t;
-                  v[i][e] = (lp_t)(oki ? t : 0.f);
+                  v[i][e] = (xe_t)(oki ? t : 0.f);
                 }
               } else {
-                v[i] = oki ? xreg4[q][i] : lpx4{};
+                v[i] = oki ? xreg4[q][i] : xe4_t{};
               }
             }
-            lp_t* xh = reinterpret_cast<lp_t*>(xs) + xlds[q];
+            xe_t* xh = reinterpret_cast<xe_t*>(xs) + xlds[q];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const lpx4 w = {v[0][e], v[1][e], v[2][e], v[3][e]};
-              *reinterpret_cast<lpx4*>(xh + e * kcp) = w;
+              const xe4_t w = {v[0][e], v[1][e], v[2][e], v[3][e]};
+              *reinterpret_cast<xe4_t*>(xh + e * kcp) = w;
             }
           }
         } else if (u < nunits) {
@@ -381,7 +428,17 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
             float v = (float)xreg[q];
             if (act_in) v = v < 0.f ? v * slope : v;
             v = ok ? v : 0.f;
-            if constexpr (BF) {
+            if constexpr (SPL) {
+              const int r = u / xw_pad;
+              const int t = u - r * xw_pad;
+              const float hf = __uint_as_float(__float_as_uint(v) & 0xffff0000u);
+              const float rr = v - hf;
+              const float mf = __uint_as_float(__float_as_uint(rr) & 0xffff0000u);
+              __bf16* xh = reinterpret_cast<__bf16*>(xs) + t * kcp + r;
+              xh[0] = (__bf16)hf;
+              xh[xpl] = (__bf16)mf;
+              xh[2 * xpl] = (__bf16)(rr - mf);
+            } else if constexpr (BF) {
               const int r = u / xw_pad;
               const int t = u - r * xw_pad;
               reinterpret_cast<xe_t*>(xs)[t * kcp + r] = (xe_t)v;
@@ -400,7 +457,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
 
   wdma(0, stage0);
   gload(0);
-  lstore(stage0, 0);
+  lstore(xbuf1, 0);
   __syncthreads();
 
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -413,7 +470,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
     }
 
     const float* ws = cur;
-    const float* xs = cur + wsz;
+    const float* xs = (ch & 1) ? xbuf2 : xbuf1;
     if constexpr (SPL) {
       // k-step = (tap j, 16 channels) as in the 16-bit path below, on fp32
       // slabs: A = two 16-byte reads of W image [j][c8][row][8], B = two of
@@ -424,7 +481,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
       const int G = kc >> 4;
       const int nsteps = k * G;
       typedef float f4 __attribute__((ext_vector_type(4)));
-      auto load = [&](int st, f32x8_t* a, f32x8_t* bb) {
+      auto load = [&](int st, f32x8_t* a, bf16x8_t* bh, bf16x8_t* bm, bf16x8_t* bl) {
         const int j = st / G;
         const int g = st - j * G;
 #pragma unroll
@@ -435,17 +492,20 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
         }
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
-          const f4* xp = reinterpret_cast<const f4*>(
-              xs + (wn + ni * 32 + l32 + j * dil + xsh) * kcp + 16 * g + 8 * lhi);
-          bb[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
+          const lpx4* xp = reinterpret_cast<const lpx4*>(
+              reinterpret_cast<const __bf16*>(xs) + (wn + ni * 32 + l32 + j * dil + xsh) * kcp +
+              16 * g + 8 * lhi);
+          const int P4 = xpl / 4;  // plane stride in 8-byte pieces
+          bh[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
+          bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+          bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
         }
       };
-      auto mma = [&](const f32x8_t* a, const f32x8_t* bb) {
-        bf16x8_t ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+      auto mma = [&](const f32x8_t* a, const bf16x8_t* bh, const bf16x8_t* bm,
+                     const bf16x8_t* bl) {
+        bf16x8_t ah[TM], am[TM], al[TM];
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi) split3_bf16(a[mi], ah[mi], am[mi], al[mi]);
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni) split3_bf16(bb[ni], bh[ni], bm[ni], bl[ni]);
         // small terms first
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
@@ -461,16 +521,17 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
             acc[mi][ni] = c;
           }
       };
-      f32x8_t a0[TM], b0[TN], a1[TM], b1[TN];
-      load(0, a0, b0);
+      f32x8_t a0[TM], a1[TM];
+      bf16x8_t bh0[TN], bm0[TN], bl0[TN], bh1[TN], bm1[TN], bl1[TN];
+      load(0, a0, bh0, bm0, bl0);
       int st = 0;
       for (; st + 2 <= nsteps; st += 2) {
-        load(st + 1, a1, b1);
-        mma(a0, b0);
-        load(st + 2, a0, b0);
-        mma(a1, b1);
+        load(st + 1, a1, bh1, bm1, bl1);
+        mma(a0, bh0, bm0, bl0);
+        load(st + 2, a0, bh0, bm0, bl0);
+        mma(a1, bh1, bm1, bl1);
       }
-      if (st < nsteps) mma(a0, b0);
+      if (st < nsteps) mma(a0, bh0, bm0, bl0);
     } else if constexpr (BF) {
       // k-step = (tap j, 16 channels): A = one 16-byte bf16x8 read per
       // 32-row fragment (W image [j][c8][row][8]); B = 8 channel rows of the
@@ -583,7 +644,12 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
       }
     }
-    if (more) lstore(nxt, (ch + 1) * kc);
+    if constexpr (SPL) {
+      __syncthreads();  // every wave is done with the (single) X buffer
+      if (more) lstore(xbuf1, (ch + 1) * kc);
+    } else {
+      if (more) lstore(nxt + wsz, (ch + 1) * kc);
+    }
     __syncthreads();
   }
 
@@ -747,14 +813,16 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     // 32-bit window offsets
     if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
       return VITS_E_UNSUP;
-    if (V4 && IO16) {  // T4 staging: kc/4 channel quads x ceil(nb/4)*4 blocks
+    if (V4 && (IO16 || SPL)) {  // T4 staging: kc/4 channel quads x ceil(nb/4)*4 blocks
       constexpr int nu = (XTile<BN, BF, IO16>::floats / 16 + 48 + 255) / 256;
       if (d.kc % 16 || (size_t)d.kc * ((xrs[i] / 4 + 3) / 4) > (size_t)nu * 256)
         return VITS_E_UNSUP;
     }
-    const size_t xslots = BF ? (SPL ? xrs[i] * (d.kc + 4) : (xrs[i] * (d.kc + 4) + 1) / 2) : xsz;
+    const size_t xslots = BF ? (SPL ? (3 * xrs[i] * (d.kc + 4) + 1) / 2 : (xrs[i] * (d.kc + 4) + 1) / 2) : xsz;
     // + tail pad: the software pipeline reads one k-step past the last chunk
-    const size_t l = sizeof(float) * (2 * (wsz + xslots) + 2 * (size_t)d.k * BM + 2 * xrs[i] + 64);
+    // (split fp32: one X buffer)
+    const size_t l = sizeof(float) * (2 * wsz + (SPL ? 1 : 2) * xslots + 2 * (size_t)d.k * BM +
+                                      2 * xrs[i] + 64);
     if (l > lds) lds = l;
     const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;
     if (x > gx) gx = x;
@@ -808,8 +876,8 @@ int launch_tile(const ConvGroup& g, hipStream_t s) {
     nv4 += v4;
     nio += d.io16 != 0;
   }
-  if (nio != 0 && (nio != g.n || !BF)) return VITS_E_UNSUP;
-  if constexpr (BF) {
+  if (nio != 0 && (nio != g.n || !BF || WT == VITS_WDT_F32S)) return VITS_E_UNSUP;
+  if constexpr (BF && WT != VITS_WDT_F32S) {  // (split fp32 has fp32 I/O only)
     if (nio) {
       if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, true>(g, s, xrs4);
       if (nv4 != 0) return VITS_E_UNSUP;

@@ -214,13 +214,13 @@ def pack_bf16(enabled: bool = True):
 def _pick_tile_f32s(m: int, k: int) -> int:
     """Split-fp32 tile (VITS_WDT_F32S), from the per-shape sweep of
     tools/conv_bench.py (WDT=3 TILES=0,1,2,3) on MI355X at B=16, Ty=500:
-    k <= 3 -> 128x128 (256/128-channel stages 126-136 TF/s vs 102-124 for
-    64x256), k = 6..8 -> 32x256 (131-135 vs 120-130), otherwise 64x256
-    (k=11: 138-144; flow k=5: 114)."""
-    if k <= 3 and m >= 128:
+    k = 3 on >= 128 rows -> 128x128 (127-140 TF/s), k <= 8 otherwise ->
+    64x128 (k=7 147-159, the polyphase upsamplers 111-117, conv_pre 135,
+    flow k=5 133), k >= 9 -> 64x256 (k=11 145-158)."""
+    if k == 3 and m >= 128:
         return TILE_128x128
-    if 6 <= k <= 8:
-        return TILE_32x256
+    if k <= 8:
+        return TILE_64x128
     return TILE_64x256
 
 
@@ -410,6 +410,14 @@ def conv_flops(desc: ConvDesc, batch: int) -> int:
     return 2 * batch * desc.m * cols * desc.cin * desc.k
 
 
+# Dense MFMA peaks (MI355X_MICROARCH.md) of the arithmetic each weight type
+# runs: exact fp32 on v_mfma_f32_32x32x2_f32 (157.3 TF/s); bf16 / fp16 ~2.5
+# PF/s; split fp32 = six bf16 MFMAs per fp32 product, 2.5 PF / 6.
+BF16_DENSE_PEAK_TFLOPS = 2500.0
+MFMA_PEAK_TFLOPS = {WDT_F32: 157.3, WDT_BF16: BF16_DENSE_PEAK_TFLOPS,
+                    WDT_F16: BF16_DENSE_PEAK_TFLOPS, WDT_F32S: BF16_DENSE_PEAK_TFLOPS / 6}
+
+
 class ConvTimer:
     """Optional per-launch timing of the conv kernel with HIP events on the
     launch stream (used by bench.py for the roofline of the dominant kernel).
@@ -420,6 +428,7 @@ class ConvTimer:
     def __init__(self):
         self.records = []  # (start_event, end_event, flops)
         self.shapes = []   # one label per record (tools/infer_breakdown.py)
+        self.peaks = []    # MFMA-bound TFLOP/s of each record's arithmetic (MFMA_PEAK)
 
     def __enter__(self):
         ConvTimer.active = self
@@ -442,6 +451,7 @@ class ConvTimer:
               "vits_conv1d_forward_groups")
         e.record(stream)
         self.records.append((s, e, sum(conv_flops(d, batch) for d in group)))
+        self.peaks.append(MFMA_PEAK_TFLOPS[group[0].wdtype])
         self.shapes.append("conv " + "+".join(
             f"m{d.m}c{d.cin}k{d.k}d{d.dil}T{d.n_out}e{d.epi}t{d.tile}" for d in group))
 
@@ -455,6 +465,7 @@ class ConvTimer:
               "vits_resblock_pair_forward")
         e.record(stream)
         self.records.append((s, e, sum(resblock_pair_flops(d, batch) for d in group)))
+        self.peaks.append(MFMA_PEAK_TFLOPS[WDT_F32])
         self.shapes.append("pair " + "+".join(
             f"C{d.channels}k{d.k}d{d.dil}T{d.t_len}" for d in group))
 
@@ -462,8 +473,13 @@ class ConvTimer:
         torch.cuda.synchronize()
         ms = [s.elapsed_time(e) for s, e, _ in self.records]
         fl = [f for _, _, f in self.records]
+        # the MFMA-bound minimum time of the same launches (each at the peak
+        # of the MFMA form its arithmetic runs on)
+        min_ms = sum(f / (pk * 1e9) for f, pk in zip(fl, self.peaks))
         return dict(launches=len(ms), total_ms=float(sum(ms)), total_flops=int(sum(fl)),
-                    avg_ms=float(sum(ms) / max(1, len(ms))))
+                    avg_ms=float(sum(ms) / max(1, len(ms))), mfma_bound_ms=float(min_ms),
+                    f32s_flops=int(sum(f for f, pk in zip(fl, self.peaks)
+                                       if pk == MFMA_PEAK_TFLOPS[WDT_F32S])))
 
     def per_launch(self):
         """[(label, ms, flops)] in launch order."""
