@@ -86,6 +86,8 @@ struct XTile {
 constexpr int VITS_W_TILE_BF = 6144;
 // split-fp32 (VITS_WDT_F32S) W stage in floats: k=11, kc=16, BM=64 fits
 constexpr int VITS_W_TILE_SPL = 11264;
+// ... and with the W chunk pre-split through registers (128x128 tiles)
+constexpr int VITS_W_TILE_WPS = 8192;
 // low-precision element type of weight type WT (VITS_WDT_BF16 / VITS_WDT_F16)
 template <int WT>
 struct LowP {
@@ -174,6 +176,14 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   // three bf16 terms in registers per fragment (split3_bf16)
   constexpr bool SPL = WT == VITS_WDT_F32S;
   constexpr int WQ = SPL ? 8 : 4;  // float slots per (W row, 8 channels)
+  // split fp32 on 128x128 tiles: the W chunk is staged pre-split as well
+  // (three bf16 planes, one buffer; global -> registers under the MFMAs,
+  // split and written between the chunk's two barriers), so the k-step
+  // loop runs no VALU split; kc*k*BM <= VITS_W_TILE_WPS
+  // (measured on MI355X: k=3 126 -> 137 TF/s on 128x128; no gain on 64x128,
+  // whose 2-tap upsamplers lose 20 %)
+  constexpr bool WPS = SPL && BM == 128 && BN == 128;
+  constexpr int NWU = VITS_W_TILE_WPS / 8 / 256;  // 8-float W entries per thread
   typedef typename LowP<WT>::T lp_t;
   typedef lp_t lpx8 __attribute__((ext_vector_type(8)));
   typedef lp_t lpx4 __attribute__((ext_vector_type(4)));
@@ -215,7 +225,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   // two stages: [W0][X0][W1][X1] (split fp32: [W0][W1][X])
   float* const stage0 = smem;
   float* const stage1 = SPL ? smem + wsz : smem + wsz + xslots;
-  float* const xbuf1 = SPL ? smem + 2 * wsz : stage0 + wsz;  // X of stage 0
+  float* const xbuf1 = WPS ? smem + 3 * wsz / 2 : SPL ? smem + 2 * wsz : stage0 + wsz;  // X of stage 0
   float* const xbuf2 = SPL ? xbuf1 : stage1 + wsz;            // X of stage 1
 
   const int b = (int)blockIdx.z - gi * G.batch;
@@ -316,6 +326,47 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
         }
         __builtin_amdgcn_global_load_lds(wsrc + (int64_t)gr * S + col,
                                          (lds_void_t)(st + q * 256), 16, 0, 0);
+      }
+    }
+  };
+  // ---- W chunk, pre-split path (WPS): global -> registers; split into the
+  // three bf16 planes [j][c8][BM][8] (plane stride wsz elements) in wstore
+  f32x8_t wreg[WPS ? NWU : 1];
+  const int nwe = kc * k * BM / 8;
+  auto wgload = [&](int c0) {
+    if constexpr (WPS) {
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      const float* wsrc = p.w + ((int64_t)(c0 / 16) * k * 2 * p.m_pad + m0) * 8;
+      const int c8n = kc >> 3;
+#pragma unroll
+      for (int q = 0; q < NWU; ++q) {
+        if (q * 256 < nwe) {
+          const int e0 = tid + q * 256;
+          const int e = e0 < nwe ? e0 : 0;
+          const int r = e / BM;
+          const int ml = e - r * BM;
+          const int j = r / c8n;
+          const int c8 = r - j * c8n;
+          const int gr = ((c8 >> 1) * k + j) * 2 + (c8 & 1);
+          const f4* src = reinterpret_cast<const f4*>(wsrc + (int64_t)gr * p.m_pad * 8 + ml * 8);
+          wreg[q] = __builtin_shufflevector(src[0], src[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+    }
+  };
+  auto wstore = [&]() {
+    if constexpr (WPS) {
+      __bf16* wh = reinterpret_cast<__bf16*>(smem);
+#pragma unroll
+      for (int q = 0; q < NWU; ++q) {
+        const int e = tid + q * 256;
+        if (q * 256 < nwe && e < nwe) {
+          bf16x8_t h, m, l;
+          split3_bf16(wreg[q], h, m, l);
+          *reinterpret_cast<bf16x8_t*>(wh + e * 8) = h;
+          *reinterpret_cast<bf16x8_t*>(wh + wsz + e * 8) = m;
+          *reinterpret_cast<bf16x8_t*>(wh + 2 * wsz + e * 8) = l;
+        }
       }
     }
   };
@@ -455,8 +506,12 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   const int half = kc >> 1;
   const int steps = k * half;  // MFMA k-steps per chunk
 
-  wdma(0, stage0);
+  if constexpr (WPS)
+    wgload(0);
+  else
+    wdma(0, stage0);
   gload(0);
+  wstore();
   lstore(xbuf1, 0);
   __syncthreads();
 
@@ -465,13 +520,73 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
     float* nxt = (ch & 1) ? stage0 : stage1;
     const bool more = ch + 1 < nchunks;
     if (more) {  // both in flight under the MFMAs below
-      wdma((ch + 1) * kc, nxt);
+      if constexpr (WPS)
+        wgload((ch + 1) * kc);
+      else
+        wdma((ch + 1) * kc, nxt);
       gload((ch + 1) * kc);
     }
 
-    const float* ws = cur;
+    const float* ws = WPS ? smem : cur;  // (WPS: one W buffer)
     const float* xs = (ch & 1) ? xbuf2 : xbuf1;
-    if constexpr (SPL) {
+    if constexpr (WPS) {
+      // both operands pre-split in LDS: A = one 16-byte read per plane of
+      // the W planes [j][c8][row][8], B as below; six MFMAs per (mi, ni)
+      const __bf16* wh = reinterpret_cast<const __bf16*>(ws);
+      const int c8n = kc >> 3;
+      const int G = kc >> 4;
+      const int nsteps = k * G;
+      auto load = [&](int st, bf16x8_t* ah, bf16x8_t* am, bf16x8_t* al, bf16x8_t* bh,
+                      bf16x8_t* bm, bf16x8_t* bl) {
+        const int j = st / G;
+        const int g = st - j * G;
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          const bf16x8_t* ap = reinterpret_cast<const bf16x8_t*>(
+              wh + ((j * c8n + 2 * g + lhi) * BM + wm + mi * 32 + l32) * 8);
+          ah[mi] = ap[0];
+          am[mi] = ap[wsz / 8];
+          al[mi] = ap[wsz / 4];
+        }
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+          const lpx4* xp = reinterpret_cast<const lpx4*>(
+              reinterpret_cast<const __bf16*>(xs) + (wn + ni * 32 + l32 + j * dil + xsh) * kcp +
+              16 * g + 8 * lhi);
+          const int P4 = xpl / 4;
+          bh[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
+          bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+          bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      };
+      auto mma = [&](const bf16x8_t* ah, const bf16x8_t* am, const bf16x8_t* al,
+                     const bf16x8_t* bh, const bf16x8_t* bm, const bf16x8_t* bl) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) {
+            f32x16 c = acc[mi][ni];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bl[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mi], bh[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mi], bm[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bm[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mi], bh[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bh[ni], c, 0, 0, 0);
+            acc[mi][ni] = c;
+          }
+      };
+      bf16x8_t ah0[TM], am0[TM], al0[TM], bh0[TN], bm0[TN], bl0[TN];
+      bf16x8_t ah1[TM], am1[TM], al1[TM], bh1[TN], bm1[TN], bl1[TN];
+      load(0, ah0, am0, al0, bh0, bm0, bl0);
+      int st = 0;
+      for (; st + 2 <= nsteps; st += 2) {
+        load(st + 1, ah1, am1, al1, bh1, bm1, bl1);
+        mma(ah0, am0, al0, bh0, bm0, bl0);
+        load(st + 2, ah0, am0, al0, bh0, bm0, bl0);
+        mma(ah1, am1, al1, bh1, bm1, bl1);
+      }
+      if (st < nsteps) mma(ah0, am0, al0, bh0, bm0, bl0);
+    } else if constexpr (SPL) {
       // k-step = (tap j, 16 channels) as in the 16-bit path below, on fp32
       // slabs: A = two 16-byte reads of W image [j][c8][row][8], B = two of
       // the [t][kcp] window; each fragment split into three bf16 terms, six
@@ -646,7 +761,10 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
     }
     if constexpr (SPL) {
       __syncthreads();  // every wave is done with the (single) X buffer
-      if (more) lstore(xbuf1, (ch + 1) * kc);
+      if (more) {
+        wstore();  // (WPS: the single W buffer too)
+        lstore(xbuf1, (ch + 1) * kc);
+      }
     } else {
       if (more) lstore(nxt + wsz, (ch + 1) * kc);
     }
@@ -807,7 +925,8 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     constexpr bool SPL = WT == VITS_WDT_F32S;
     const size_t wsz = (BF && !SPL) ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
     const size_t xsz = (size_t)d.kc * xrs[i];
-    if (wsz > (size_t)(SPL ? VITS_W_TILE_SPL : BF ? VITS_W_TILE_BF : VITS_W_TILE) ||
+    if (wsz > (size_t)(SPL ? (BM == 128 && BN == 128 ? VITS_W_TILE_WPS : VITS_W_TILE_SPL)
+                           : BF ? VITS_W_TILE_BF : VITS_W_TILE) ||
         xsz > (size_t)XTile<BN, BF, IO16>::floats)
       return VITS_E_UNSUP;
     // 32-bit window offsets
@@ -821,7 +940,8 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     const size_t xslots = BF ? (SPL ? (3 * xrs[i] * (d.kc + 4) + 1) / 2 : (xrs[i] * (d.kc + 4) + 1) / 2) : xsz;
     // + tail pad: the software pipeline reads one k-step past the last chunk
     // (split fp32: one X buffer)
-    const size_t l = sizeof(float) * (2 * wsz + (SPL ? 1 : 2) * xslots + 2 * (size_t)d.k * BM +
+    const size_t wst = (SPL && BM == 128 && BN == 128) ? 3 * wsz / 2 : 2 * wsz;  // W stage(s)
+    const size_t l = sizeof(float) * (wst + (SPL ? 1 : 2) * xslots + 2 * (size_t)d.k * BM +
                                       2 * xrs[i] + 64);
     if (l > lds) lds = l;
     const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;

@@ -213,10 +213,11 @@ def pack_bf16(enabled: bool = True):
 
 def _pick_tile_f32s(m: int, k: int) -> int:
     """Split-fp32 tile (VITS_WDT_F32S), from the per-shape sweep of
-    tools/conv_bench.py (WDT=3 TILES=0,1,2,3) on MI355X at B=16, Ty=500:
-    k = 3 on >= 128 rows -> 128x128 (127-140 TF/s), k <= 8 otherwise ->
-    64x128 (k=7 147-159, the polyphase upsamplers 111-117, conv_pre 135,
-    flow k=5 133), k >= 9 -> 64x256 (k=11 145-158)."""
+    tools/conv_bench.py (WDT=3 TILES=0,1,2,3) on MI355X at B=16, Ty=500
+    (profiles/r02_split_conv_sweep.txt): k = 3 on >= 128 rows -> 128x128
+    (W pre-split too, 131-140 TF/s), k <= 8 otherwise -> 64x128 (k=7
+    147-159, the polyphase upsamplers 111-117, conv_pre 135, flow k=5 133),
+    k >= 9 -> 64x256 (k=11 145-158)."""
     if k == 3 and m >= 128:
         return TILE_128x128
     if k <= 8:
