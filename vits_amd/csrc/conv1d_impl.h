@@ -941,8 +941,13 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     // + tail pad: the software pipeline reads one k-step past the last chunk
     // (split fp32: one X buffer)
     const size_t wst = (SPL && BM == 128 && BN == 128) ? 3 * wsz / 2 : 2 * wsz;  // W stage(s)
-    const size_t l = sizeof(float) * (wst + (SPL ? 1 : 2) * xslots + 2 * (size_t)d.k * BM +
-                                      2 * xrs[i] + 64);
+    // split fp32 ([W0][W1][X] / [W][X]): a W read-ahead lands in the next W
+    // stage or in X; only the B read-ahead of the last plane runs past the
+    // end, by < (dil + 2) window rows of kc + 4 bf16 - a tail that keeps the
+    // k=7, d=5 64x128 tile at two workgroups per CU
+    const size_t tail = SPL ? (size_t)(d.dil + 2) * (d.kc + 4) / 2 + 64
+                            : 2 * (size_t)d.k * BM + 2 * xrs[i] + 64;
+    const size_t l = sizeof(float) * (wst + (SPL ? 1 : 2) * xslots + tail);
     if (l > lds) lds = l;
     const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;
     if (x > gx) gx = x;
