@@ -1048,6 +1048,11 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
                                                                     : XTile<128, BF>::floats);
       }
       if (blocks < 512 && fits128) return launch_tile<64, 128, 2, 2, WT>(g, s);
+      if constexpr (WT == VITS_WDT_F32S) {
+        // split fp32: 2x2 waves (32x128 per wave) - each A-fragment split
+        // feeds four B fragments instead of two (k=11 convs +1..3 %)
+        return launch_tile<64, 256, 2, 2, WT>(g, s);
+      }
       return launch_tile<64, 256, 1, 4, WT>(g, s);
     }
     case VITS_TILE_32x256:
