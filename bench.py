@@ -342,7 +342,24 @@ def train_cpu_baseline(budget_s=10.0, B=4, max_steps=50):
                       "(vits_amd.train.TrainStep, MAS/neg_cent from oracle/, torch.stft)"}
 
 
-def train_leg(args, device, rank, world, dist):
+TRAIN_GFLOP_PER_UTT = 365.4  # FlopCounterMode, train_stft step, Tx=100 Ty=500
+FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 / bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def train_traffic():
+    """HBM bytes per train step from the newest committed train PMC summary
+    (profiles/<tag>_train_summary.json, tools/summarize_train_profiles.py)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_train_summary.json")))
+    if not files:
+        return None, None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return (d.get("hbm_bytes_per_step"), d.get("batch"), os.path.relpath(files[-1], ROOT))
+
+
+def train_leg(args, device, rank, world, dist, B=None, cpu_base=True):
     """Timed train_stft steps (BASELINE C3/C4) on synthetic base.json batches."""
     from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
 
@@ -356,7 +373,7 @@ def train_leg(args, device, rank, world, dist):
     use_graph = not args.train_eager
     st = TrainStep(hps, net_g, net_d, device, ddp=world > 1 and not use_graph,
                    capturable=use_graph, allreduce=world > 1 and use_graph)
-    B = args.train_batch
+    B = B or args.train_batch
     batch = [t.to(device) for t in synthetic_batch(hps, B, tx=args.tx, ty=args.ty, seed=rank)]
     graph_err = None
     if use_graph:
@@ -394,16 +411,55 @@ def train_leg(args, device, rank, world, dist):
            "parallelism": (f"dp{world} (flat RCCL all-reduce per network)" if st.allreduce else
                            f"ddp{world} (RCCL all-reduce)") if world > 1 else "single GPU",
            "graph": use_graph,
-           "tflops_alg": round(365.4e9 * utt / el / 1e12, 2),
+           "tflops_alg": round(TRAIN_GFLOP_PER_UTT * 1e9 * utt / el / 1e12, 2),
            "loss_gen_all": round(float(out["loss_gen_all"]), 4),
            "reference_cpu": "0.945 utt/s at B=4 on 8 vCPU (BASELINE.md, measured in the survey)"}
+    # roofline of the whole step: algorithmic FLOPs (365.4 GFLOP per
+    # utterance) per GPU-second against the dense fp16 MFMA peak; traffic =
+    # PMC HBM bytes per step (FETCH x2 + WRITE over every kernel of one
+    # replayed step, scaled to this batch) from the committed summary
+    achieved = TRAIN_GFLOP_PER_UTT * 1e9 * B * args.train_steps / el / 1e12
+    tb, tbatch, tsrc = train_traffic()
+    res["roofline"] = {
+        "bound": "mfma", "kernel": "whole train_stft step (every kernel of the replayed graph)",
+        "achieved": round(achieved, 2), "peak": FP16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / FP16_MFMA_PEAK_TFLOPS, 4),
+        "traffic": None if tb is None else int(tb * B / tbatch),
+        "traffic_unit": "HBM bytes per step (PMC, scaled from batch %s)" % tbatch,
+        "traffic_source": tsrc}
     if graph_err:
         res["graph_error"] = graph_err
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_base:
         res["cpu_baseline"] = train_cpu_baseline()
     del st, net_g, net_d
     torch.cuda.empty_cache()
     return res
+
+
+def conv_kernel_table(timer, steps):
+    """Per-shape rows of the headline step's conv launches (the "kernel,
+    TF/s, fraction of ceiling" table): launches grouped by descriptor label
+    (rows m, input channels c, taps k, dilation d, output length T, epilogue
+    e, tile t), each against the MFMA peak of its arithmetic (exact f32
+    157.3, split f32 416.7, bf16 2500 TF/s).  Sorted by time per step."""
+    from vits_amd.ops import MFMA_PEAK_TFLOPS, WDT_F32S
+
+    rows = {}
+    torch.cuda.synchronize()
+    for lab, (s, e, fl), pk in zip(timer.shapes, timer.records, timer.peaks):
+        r = rows.setdefault(lab, [0, 0.0, 0, pk])
+        r[0] += 1
+        r[1] += s.elapsed_time(e)
+        r[2] += fl
+    out = []
+    for lab, (n, ms, fl, pk) in sorted(rows.items(), key=lambda kv: -kv[1][1]):
+        tf = fl / (ms * 1e9)
+        kind = ("split-f32" if pk == MFMA_PEAK_TFLOPS[WDT_F32S] else
+                "exact-f32" if pk < 200 else "16-bit")
+        out.append({"kernel": lab, "arith": kind, "launches_per_step": round(n / steps, 2),
+                    "ms_per_step": round(ms / steps, 4), "achieved": round(tf, 1),
+                    "unit": "TFLOP/s", "peak": round(pk, 1), "frac": round(tf / pk, 3)})
+    return out
 
 
 def fp32_arith() -> str:
@@ -415,6 +471,53 @@ def fp32_arith() -> str:
             "bf16 terms, six bf16 MFMAs per product, fp32 accumulation (error vs fp64 at or "
             "below the exact-f32 kernel's, tests/test_kernels_gpu.py); the 32/64-channel "
             "stages exact f32")
+
+
+def _launch_ranks(args) -> int:
+    """``--gpus N`` (N > 1) without a torchrun environment: start N ranks as
+    ``python -m torch.distributed.run`` in a CHILD process - this process
+    never touches the GPU - and exit with its status.  Rank 0 prints the
+    JSON line (its stdout is passed through)."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run_line(args, world, rank, dist):
+    """--dry-run: the launcher / rank / aggregation logic without a GPU
+    (gloo, a small CPU matmul as the "step"); same fields as the real line."""
+    x = torch.randn(256, 256)
+    for _ in range(args.warmup):
+        x @ x
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x @ x
+    if dist:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    B, Ty = args.batch, args.ty
+    return {"metric": METRIC, "value": round(args.steps * B * Ty * HOP * world / el, 1),
+            "unit": "output samples/s", "n_gpus": world, "rank_seen": rank, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "dry run (CPU, no GPU work)",
+            "config": {"workload": "dry run", "global_batch": B * world, "seq_len": Ty,
+                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU"}}
 
 
 def main():
@@ -430,7 +533,9 @@ def main():
                     help="fp32 conv arithmetic (vits_amd.engine.FP32_MODE; default split)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--train-batch", type=int, default=32)
+    ap.add_argument("--train-batch", type=int, default=32, help="C4: utterances per GPU")
+    ap.add_argument("--train-batch-c3", type=int, default=64,
+                    help="C3: the one-GPU train_stft batch (0: skip)")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--train-warmup", type=int, default=2)
     ap.add_argument("--no-train", action="store_true")
@@ -438,24 +543,48 @@ def main():
                     help="time the eager train step instead of the captured hipGraph")
     ap.add_argument("--no-longform", action="store_true")
     ap.add_argument("--no-kernels", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU-only check of the rank launcher / aggregation (gloo, no GPU work)")
     args = ap.parse_args()
     if args.fp32_mode:  # read by vits_amd.engine at import
         os.environ["VITS_FP32_MODE"] = args.fp32_mode
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not under torchrun: start the N ranks ourselves (before any GPU use)
+        sys.exit(_launch_ranks(args))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} ranks",
+              file=sys.stderr)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank)
+        if not args.dry_run:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo" if args.dry_run else "nccl", init_method="env://",
+                                world_size=world, rank=rank)
+    if args.dry_run:
+        line = dry_run_line(args, world, rank, dist)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     device = torch.device("cuda", local_rank)
 
-    # the train leg runs first, on a clean allocator (its MIOpen algorithm
-    # choice depends on free workspace), and releases its memory afterwards
-    train = None if args.no_train else train_leg(args, device, rank, world, dist)
+    # the train legs run first, on a clean allocator (its MIOpen algorithm
+    # choice depends on free workspace), and release their memory afterwards:
+    # C4 = --train-batch per GPU (32, weak scaling over the ranks), and at
+    # one rank also C3 = the train_stft step at batch 64 on one GPU
+    train = train_c3 = None
+    if not args.no_train:
+        train = train_leg(args, device, rank, world, dist, args.train_batch)
+        if world == 1 and args.train_batch_c3 and args.train_batch_c3 != args.train_batch:
+            train_c3 = train_leg(args, device, rank, world, dist, args.train_batch_c3,
+                                 cpu_base=False)
 
     model = build_model(device)
     B, Tx, Ty = args.batch, args.tx, args.ty
@@ -485,6 +614,7 @@ def main():
         elapsed = time.perf_counter() - t0
 
         roof = None
+        kernel_table = []
         if not args.no_roofline and not args.graph:
             from vits_amd.ops import ConvTimer
 
@@ -499,6 +629,7 @@ def main():
             # rate of the MFMA-bound minimum time of the same launches
             peak = (s["total_flops"] / 1e12) / (s["mfma_bound_ms"] / 1e3)
             traffic, tsrc = pmc_traffic()
+            kernel_table = conv_kernel_table(timer, args.steps)
             roof = {"bound": "mfma",
                     "kernel": "conv1d_mfma_kernel + resblock_pair_kernel (every conv / fused "
                               "ResBlock2-pair launch of a step)",
@@ -517,6 +648,18 @@ def main():
 
     longform = None if args.no_longform else longform_leg(model, device, rank)
     kern = None if args.no_kernels else kernels_leg(device)
+    if kern:
+        for name, k in kern.items():
+            if not isinstance(k, dict):
+                continue
+            if "TFLOPs" in k:
+                kernel_table.append({"kernel": name, "shape": k["shape"], "ms": k["ms"],
+                                     "achieved": k["TFLOPs"], "unit": "TFLOP/s",
+                                     "peak": FP32_MFMA_PEAK_TFLOPS, "frac": k["frac_fp32_mfma"]})
+            elif "GBps" in k:
+                kernel_table.append({"kernel": name, "shape": k["shape"], "ms": k["ms"],
+                                     "achieved": k["GBps"], "unit": "GB/s", "peak": 8000.0,
+                                     "frac": k["frac_hbm"], "bound": k.get("bound", "hbm")})
     latency = None if args.no_kernels else latency_leg(model, device)
 
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
@@ -549,6 +692,8 @@ def main():
             "kernels": kern,
             "latency_b1": latency,
             "train": train,
+            "train_c3": train_c3,
+            "kernel_table": kernel_table,
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(model, Tx, Ty)

@@ -123,3 +123,52 @@ def test_cpu_radam_matches_radam_py(wd):
     ref = radam_ref(params, grads, lr=1e-3, wd=wd)
     for p, r in zip(ps, ref):
         assert torch.allclose(p.detach(), r, rtol=0, atol=1e-7 * r.abs().max().item())
+
+
+def test_tensor_lr_checkpoint_is_portable_and_loads_in_place(tmp_path):
+    """a checkpoint written from an optimizer whose lr is a
+    tensor (the graph-capturable TrainStep) stores floats, so a float-lr
+    optimizer (the reference's) loads it; loading INTO a pinned tensor-lr
+    optimizer keeps the lr / initial_lr / moment tensor objects (a captured
+    graph reads them) and copies the loaded values in, and a scheduler
+    step afterwards continues the loaded sequence in place."""
+    from vits_amd import utils
+
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(5, 3))
+    lr_t = torch.tensor(2e-4)
+    opt = torch.optim.AdamW([w], lr_t, betas=(0.8, 0.99), foreach=False)
+    sched = torch.optim.lr_scheduler.ExponentialLR(opt, 0.5)
+    w.grad = torch.randn(5, 3)
+    opt.step()
+    sched.step()  # lr 1e-4
+    utils.save_checkpoint(torch.nn.Linear(1, 1), opt, 3, str(tmp_path / "G_3.pth"))
+    sd = torch.load(tmp_path / "G_3.pth", weights_only=True)["optimizer"]
+    assert isinstance(sd["param_groups"][0]["lr"], float)
+    assert isinstance(sd["param_groups"][0]["initial_lr"], float)
+    # a float-lr optimizer (the reference's AdamW, default foreach) consumes it
+    w2 = torch.nn.Parameter(torch.randn(5, 3))
+    ref = torch.optim.AdamW([w2], 2e-4, betas=(0.8, 0.99))
+    ref.load_state_dict(sd)
+    w2.grad = torch.randn(5, 3)
+    ref.step()
+    assert abs(ref.param_groups[0]["lr"] - 1e-4) < 1e-10  # an fp32 tensor lr, stored as float
+
+    # loading into a pinned tensor-lr optimizer: objects kept, values copied
+    w3 = torch.nn.Parameter(torch.randn(5, 3))
+    lr3 = torch.tensor(7e-4)
+    opt3 = utils.pin_optimizer_state(torch.optim.AdamW([w3], lr3, betas=(0.8, 0.99),
+                                                       foreach=False))
+    sched3 = torch.optim.lr_scheduler.ExponentialLR(opt3, 0.5)
+    w3.grad = torch.randn(5, 3)
+    opt3.step()  # creates the moments the "graph" would hold
+    m_obj = opt3.state[w3]["exp_avg"]
+    init_obj = opt3.param_groups[0]["initial_lr"]
+    sd = torch.load(tmp_path / "G_3.pth", weights_only=True)["optimizer"]  # ref.step mutated it
+    opt3.load_state_dict(sd)
+    assert opt3.param_groups[0]["lr"] is lr3 and abs(float(lr3) - 1e-4) < 1e-10
+    assert opt3.param_groups[0]["initial_lr"] is init_obj and abs(float(init_obj) - 2e-4) < 1e-10
+    assert opt3.state[w3]["exp_avg"] is m_obj
+    assert torch.equal(m_obj, opt.state[w]["exp_avg"])
+    sched3.step()
+    assert opt3.param_groups[0]["lr"] is lr3 and abs(float(lr3) - 5e-5) < 1e-10

@@ -8,6 +8,8 @@ import torch
 
 from common import build_model, tiny_cfg
 
+HERE = os.path.dirname(os.path.abspath(__file__))
+
 
 def _write_ckpts(tmp_path, n=3):
     c = tiny_cfg()
@@ -100,3 +102,29 @@ def test_emovits_graph_cache_matches_eager(tmp_path, device):
         wav, _ = tts.infer(1, text, emo)
         outs.append(wav)
     assert outs[0].shape == outs[1].shape and np.array_equal(outs[0], outs[1])
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """bench.py --gpus 2 outside torchrun starts two ranks itself (a child
+    torch.distributed.run; gloo in --dry-run) and rank 0 reports the
+    whole-job fields: n_gpus 2, global_batch 2 x batch, value over both."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(HERE)
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--steps", "3", "--warmup", "1", "--batch", "5"], capture_output=True,
+                       text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["rank_seen"] == 0
+    assert line["config"]["global_batch"] == 10
+    assert line["config"]["parallelism"] == "replicas x2"
+    one = line["value"] / 2
+    assert line["value"] == pytest.approx(3 * 5 * 500 * 192 * 2 / (line["ms_per_step"] * 3 / 1e3),
+                                          rel=1e-2) and one > 0

@@ -53,14 +53,36 @@ class FusedRAdam(torch.optim.Optimizer):
             self._scal[gi] = s
         return s
 
+    def state_dict(self):
+        """torch's state_dict with radam.py's types: each ``step`` a Python
+        int (radam.py:69 counts with ``+= 1``), a tensor ``lr`` as a float,
+        so a ``D_*.pth`` written here loads into the reference's RAdam."""
+        sd = super().state_dict()
+        for st in sd["state"].values():
+            if isinstance(st.get("step"), torch.Tensor):
+                st["step"] = int(round(float(st["step"])))
+        for g in sd["param_groups"]:
+            for k in ("lr", "initial_lr"):
+                if isinstance(g.get(k), torch.Tensor):
+                    g[k] = float(g[k])
+        return sd
+
     def load_state_dict(self, state_dict):
         """torch's load, then seed each group's device step counter from the
         loaded per-parameter ``step`` (tensor or int, all equal within a
         group as radam.py steps them together) and re-point every state's
-        ``step`` at the counter view."""
+        ``step`` at the counter view.  The counter and the moments are
+        written IN PLACE when they already exist (a captured step keeps
+        pointing at them), and a tensor ``lr`` keeps its object
+        (the loaded value is copied into it)."""
+        old = {p: dict(self.state[p]) for p in self.state}
+        old_lr = [(g.get("lr"), g.get("initial_lr")) for g in self.param_groups]
         super().load_state_dict(state_dict)
-        self._scal = {}
         for gi, group in enumerate(self.param_groups):
+            for k, prev in zip(("lr", "initial_lr"), old_lr[gi]):
+                if isinstance(prev, torch.Tensor) and k in group and group[k] is not prev:
+                    prev.fill_(float(group[k]))
+                    group[k] = prev
             steps = [self.state[p]["step"] for p in group["params"]
                      if p in self.state and "step" in self.state[p]]
             if not steps:
@@ -75,7 +97,12 @@ class FusedRAdam(torch.optim.Optimizer):
                     st["step"] = scal[0:1]
                     for k in ("exp_avg", "exp_avg_sq"):
                         if k in st:
-                            st[k] = st[k].to(device=p.device, dtype=torch.float32).contiguous()
+                            new = st[k].to(device=p.device, dtype=torch.float32).contiguous()
+                            prev = old.get(p, {}).get(k)
+                            if isinstance(prev, torch.Tensor) and prev.shape == new.shape:
+                                prev.copy_(new)
+                                new = prev
+                            st[k] = new
 
     @staticmethod
     def _lr_args(group, dev):

@@ -104,6 +104,11 @@ class TrainStep:
             self.optim_d = RAdam(net_d.parameters(), 1e-4)
         # train_stft.py:127-128 / train.py:135-136; stepped once per epoch by
         # the caller (end_epoch(), train_stft.py:138-139)
+        if self.capturable:
+            # a checkpoint load (utils.load_checkpoint -> load_state_dict)
+            # writes into the lr / moment tensors the captured graph reads
+            utils.pin_optimizer_state(self.optim_g)
+            utils.pin_optimizer_state(self.optim_d)
         self.scheduler_g = torch.optim.lr_scheduler.ExponentialLR(
             self.optim_g, gamma=hps.train.lr_decay, last_epoch=-1)
         self.scheduler_d = torch.optim.lr_scheduler.ExponentialLR(
@@ -218,8 +223,11 @@ class TrainStep:
             self.scaler.step(self.optim_g)
             self.scaler.update()
         return {"loss_disc": loss_disc.detach(), "loss_gen_all": loss_gen_all.detach(),
-                "loss_stft": loss_stft.detach(), "loss_dur": loss_dur.detach(),
-                "loss_kl": loss_kl.detach(), "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
+                "loss_gen": loss_gen.detach(), "loss_stft": loss_stft.detach(),
+                "loss_dur": loss_dur.detach(), "loss_kl": loss_kl.detach(),
+                "loss_kl_q": loss_kl_q.detach(), "sc_loss": sc_loss.detach(),
+                "mag_loss": mag_loss.detach(), "grad_norm_g": grad_norm_g,
+                "grad_norm_d": grad_norm_d}
 
     def _step_mel(self, batch):
         """One iteration of train.py's loop (train.py:171-233; the unused

@@ -126,15 +126,69 @@ def load_checkpoint(checkpoint_path, model, optimizer=None, *, adapt=False):
     return model, optimizer, iteration
 
 
+def portable_optimizer_state(optimizer):
+    """``optimizer.state_dict()`` with every param group's ``lr`` /
+    ``initial_lr`` as a Python float: a graph-capturable TrainStep keeps its
+    learning rates as device tensors, which the reference's optimizers cannot
+    consume (radam.py:92 passes ``-step_size * group['lr']`` as a number;
+    torch's foreach AdamW rejects a tensor lr without capturable)."""
+    sd = optimizer.state_dict()
+    for g in sd["param_groups"]:
+        for k in ("lr", "initial_lr"):
+            if isinstance(g.get(k), torch.Tensor):
+                g[k] = float(g[k])
+    return sd
+
+
+def pin_optimizer_state(optimizer):
+    """Make ``optimizer.load_state_dict`` write IN PLACE into the tensors a
+    captured hipGraph reads: a tensor ``lr`` / ``initial_lr`` keeps its object
+    (the loaded value is copied into it) and existing state tensors (moments,
+    device step counters) receive the loaded values instead of being
+    replaced.  Without this a resumed run (load_checkpoint, then capture or
+    an earlier capture replayed) would bake the checkpoint's float lr into
+    the graph or update orphaned moments."""
+    snap = {}
+
+    def pre(opt, state_dict):
+        snap["lr"] = [(g.get("lr"), g.get("initial_lr")) for g in opt.param_groups]
+        snap["state"] = {p: dict(st) for p, st in opt.state.items()}
+        return None
+
+    def post(opt):
+        for g, (lr, ilr) in zip(opt.param_groups, snap.get("lr", [])):
+            for k, prev in (("lr", lr), ("initial_lr", ilr)):
+                if isinstance(prev, torch.Tensor) and k in g and g[k] is not prev:
+                    prev.fill_(float(g[k]))
+                    g[k] = prev
+        for p, st in opt.state.items():
+            old = snap.get("state", {}).get(p, {})
+            for k, new in list(st.items()):
+                prev = old.get(k)
+                if isinstance(prev, torch.Tensor) and prev is not new:
+                    if isinstance(new, torch.Tensor) and new.numel() == prev.numel():
+                        prev.copy_(new.reshape(prev.shape))
+                        st[k] = prev
+                    elif not isinstance(new, torch.Tensor) and prev.numel() == 1:
+                        prev.fill_(float(new))
+                        st[k] = prev
+        snap.clear()
+
+    optimizer.register_load_state_dict_pre_hook(pre)
+    optimizer.register_load_state_dict_post_hook(post)
+    return optimizer
+
+
 def save_checkpoint(model, optimizer, iteration, checkpoint_path):
-    """``utils.py:47-57``: ``{'model', 'iteration', 'optimizer'}``."""
+    """``utils.py:47-57``: ``{'model', 'iteration', 'optimizer'}`` (learning
+    rates stored as floats, ``portable_optimizer_state``)."""
     logger.info("Saving model and optimizer state at iteration %s to %s",
                 iteration, checkpoint_path)
     torch.save(
         {
             "model": _unwrap(model).state_dict(),
             "iteration": iteration,
-            "optimizer": optimizer.state_dict() if optimizer is not None else None,
+            "optimizer": portable_optimizer_state(optimizer) if optimizer is not None else None,
         },
         checkpoint_path,
     )
@@ -355,6 +409,21 @@ def deterministic_fill_(module: torch.nn.Module, seed: int = 1234) -> torch.nn.M
     """Overwrite every parameter (not buffers) of ``module`` by key."""
     for key, p in module.named_parameters():
         p.copy_(deterministic_tensor(key, p.shape, seed).to(p.device, p.dtype))
+    return module
+
+
+@torch.no_grad()
+def deterministic_fill_sn_(module: torch.nn.Module, seed: int = 1234) -> torch.nn.Module:
+    """Overwrite the spectral-norm power-iteration buffers (``*_u`` / ``*_v``
+    beside a ``*_orig`` parameter, torch.nn.utils.spectral_norm) by key with
+    unit vectors, so a reference module and this one start their power
+    iterations from the same state (mrd.py's D, train_stft.py:86)."""
+    params = dict(module.named_parameters())
+    for key, b in module.named_buffers():
+        stem, _, leaf = key.rpartition("_")
+        if leaf in ("u", "v") and stem + "_orig" in params:
+            t = deterministic_tensor(key, b.shape, seed).double()
+            b.copy_((t / t.norm().clamp_min(1e-12)).to(b.device, b.dtype))
     return module
 
 
