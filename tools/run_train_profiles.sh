@@ -1,13 +1,14 @@
 #!/bin/bash
 # PMC HBM traffic + kernel trace of ONE captured train_stft step (run on the GPU box).
-# Each quantity is measured with R=1 and R=5 replays; per step = (R5 - R1) / 4.
+# Each quantity is measured with R=1 and R=2 replays; per step = R2 - R1.
 set -e
 TAG=${1:-r03}
 B=${2:-32}
 OUT=gpurun_out/prof_${TAG}_train
 export TMPDIR=/tmp
 mkdir -p $OUT
-for R in 1 5; do
+for R in 1 2; do
+  echo "pass R=$R"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace$R -o run -- \
     python3 tools/train_pmc.py --batch $B --replays $R > $OUT/trace$R.log 2>&1
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch$R -o run -- \

@@ -1,7 +1,7 @@
 """Summarise tools/run_train_profiles.sh into profiles/<tag>_train_summary.json
-(+ profiles/<tag>_train_kernel_stats.csv: the R=5 run's --stats table).
+(+ profiles/<tag>_train_kernel_stats.csv: the R=2 run's --stats table).
 
-Per step = (counters of the R=5 run - counters of the R=1 run) / 4, over
+Per step = counters of the R=2 run - counters of the R=1 run, over
 every kernel dispatch.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE
 and WRITE_SIZE are KiB; FETCH_SIZE is doubled (gfx950 reports half of a wide
 coalesced read stream); WRITE_SIZE is used as is.  The per-family table
@@ -50,13 +50,13 @@ def diff(a, b, scale):
     return {k: (b.get(k, 0.0) - a.get(k, 0.0)) * scale for k in set(a) | set(b)}
 
 
-f = diff(counters("fetch1"), counters("fetch5"), 2.0 * 1024 / 4)
-w = diff(counters("write1"), counters("write5"), 1024 / 4)
-t1, t5 = trace("trace1"), trace("trace5")
+f = diff(counters("fetch1"), counters("fetch2"), 2.0 * 1024)
+w = diff(counters("write1"), counters("write2"), 1024.0)
+t1, t5 = trace("trace1"), trace("trace2")
 fams = {}
 for k in set(t1) | set(t5):
-    calls = (t5.get(k, [0, 0])[0] - t1.get(k, [0, 0])[0]) / 4
-    ns = (t5.get(k, [0, 0.0])[1] - t1.get(k, [0, 0.0])[1]) / 4
+    calls = t5.get(k, [0, 0])[0] - t1.get(k, [0, 0])[0]
+    ns = t5.get(k, [0, 0.0])[1] - t1.get(k, [0, 0.0])[1]
     if calls <= 0 and ns <= 0:
         continue
     fams[k] = {"dispatches_per_step": round(calls, 1), "ms_per_step": round(ns / 1e6, 3),
@@ -71,12 +71,12 @@ summary = {"tag": tag, "batch": batch, "hbm_bytes_per_step": round(hbm),
            "hbm_write_bytes_per_step": round(sum(w.values())),
            "dispatches_per_step": round(sum(v["dispatches_per_step"] for v in fams.values()), 1),
            "kernel_ms_per_step": round(tot_ms, 3),
-           "note": "(R=5 replays - R=1 replay) / 4 of the captured train_stft step; FETCH_SIZE x2 "
+           "note": "(R=2 replays - R=1 replay) of the captured train_stft step; FETCH_SIZE x2 "
                    "(gfx950 wide-read correction), KiB->B",
            "families": dict(sorted(fams.items(), key=lambda kv: -kv[1]["ms_per_step"]))}
 os.makedirs("profiles", exist_ok=True)
 with open(os.path.join("profiles", f"{tag}_train_summary.json"), "w") as fh:
     json.dump(summary, fh, indent=1)
-shutil.copy(os.path.join(src, "trace5", "run_kernel_stats.csv"),
+shutil.copy(os.path.join(src, "trace2", "run_kernel_stats.csv"),
             os.path.join("profiles", f"{tag}_train_kernel_stats.csv"))
 print(json.dumps({k: v for k, v in summary.items() if k != "families"}, indent=1))

@@ -1,6 +1,6 @@
 """Run the captured train_stft step R times (tools/run_train_profiles.sh
-profiles this under rocprofv3 twice, with R=1 and R=5, and takes the
-difference / 4 as the per-step kernel counters, which removes the eager
+profiles this under rocprofv3 twice, with R=1 and R=2, and takes the
+difference as the per-step kernel counters, which removes the eager
 warm-up and the capture from the count)."""
 import argparse
 import os
@@ -24,11 +24,13 @@ def main():
     g, d = build_models(hps, dev)
     st = TrainStep(hps, g, d, dev, capturable=True)
     batch = [t.to(dev) for t in synthetic_batch(hps, a.batch, seed=0)]
+    print("capturing", flush=True)
     st.capture(batch, warmup=1)
     torch.cuda.synchronize()
-    for _ in range(a.replays):
+    for i in range(a.replays):
         out = st.replay()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        print("replay", i, flush=True)
     print("replays", a.replays, "loss_gen_all", float(out["loss_gen_all"]), flush=True)
 
 
