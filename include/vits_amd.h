@@ -147,6 +147,11 @@ typedef struct vits_conv1d_desc {
 #define VITS_WDT_BF16 1
 #define VITS_WDT_F16 2
 #define VITS_WDT_F32S 3
+/* VITS_WDT_F32P: the F32S arithmetic with w = the host-split bf16 planes   */
+/* [cin_pad/16][k][2][3][m_pad][8] (plane 0 = hi, 1 = mid, 2 = lo of each   */
+/* fp32 weight, x == hi + mid + lo exactly), kc 16 or 32; A fragments are  */
+/* read from global memory, so only the input window is staged in LDS.     */
+#define VITS_WDT_F32P 4
 
 int vits_conv1d_forward(const vits_conv1d_desc* d, int batch, void* stream);
 

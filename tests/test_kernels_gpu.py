@@ -97,12 +97,54 @@ def test_conv1d_split_f32_matches_exact_f32_error(device, C, k, dil, T):
     for wdt in (ops.WDT_F32, ops.WDT_F32S):
         with ops.pack_lowp(wdt):
             layer = ops.pack_conv(w.float().to(device), None, dilation=dil)
-        assert layer.wdtype == wdt
+        assert layer.wdtype == (ops.WDT_F32P if wdt == ops.WDT_F32S and ops.SPLIT_W else wdt)
         out = ops.conv1d(x.float().to(device), layer).double().cpu()
         e = out - ref
         errs[wdt] = (e.pow(2).mean().sqrt().item() / rms, e.abs().max().item() / rms)
     assert errs[ops.WDT_F32S][0] <= 1.5 * errs[ops.WDT_F32][0], errs
     assert errs[ops.WDT_F32S][1] <= 1.5 * errs[ops.WDT_F32][1], errs
+
+
+@pytest.mark.parametrize("kind,cin,cout,k,dil,T", [
+    ("store", 256, 256, 11, 5, 4000), ("store", 128, 256, 3, 1, 1001), ("gate", 128, 128, 7, 3, 2400),
+    ("gate", 256, 512, 5, 1, 500), ("store", 96, 256, 1, 1, 130), ("up", 512, 256, 16, 8, 60),
+    ("up", 256, 128, 12, 6, 403), ("store", 192, 512, 7, 1, 77), ("gate", 256, 256, 11, 1, 333)])
+def test_conv1d_presplit_weights_bitwise_equal_f32s(device, monkeypatch, kind, cin, cout, k, dil,
+                                                     T):
+    """VITS_WDT_F32P (weights split once on the host into bf16 planes, A
+    fragments from global memory, X-only LDS) runs the same six MFMAs in the
+    same order as VITS_WDT_F32S (weights split per fragment in registers):
+    the outputs must be bitwise identical - over both staging paths (T % 4
+    == 0: 16-byte blocks; otherwise element-wise), gate / store /
+    upsample epilogues, residual and cond inputs, and every tile the
+    dispatcher picks (incl. the small-grid 64x128 fallback)."""
+    g = torch.Generator().manual_seed(cin + k + T)
+    B = 2
+    x = torch.randn(B, cin, T, generator=g).to(device)
+    bias = torch.randn(cout, generator=g).to(device)
+    outs = {}
+    for split_w in (False, True):
+        monkeypatch.setattr(ops, "SPLIT_W", split_w)
+        with ops.pack_lowp(ops.WDT_F32S):
+            if kind == "up":
+                w = torch.randn(cin, cout, k, generator=torch.Generator().manual_seed(1)) * 0.05
+                layer = ops.pack_conv_transpose(w.to(device), torch.zeros(cout, device=device),
+                                                dil, (k - dil) // 2)
+            else:
+                w = torch.randn(cout, cin, k, generator=torch.Generator().manual_seed(1)) * 0.05
+                layer = ops.pack_conv(w.to(device), bias, dilation=dil, gate=kind == "gate")
+        assert layer.wdtype == (ops.WDT_F32P if split_w else ops.WDT_F32S)
+        if kind == "gate":
+            cond = torch.randn(B, cout, generator=torch.Generator().manual_seed(2)).to(device)
+            outs[split_w] = ops.conv1d(x, layer, in_slope=0.1, cond=cond)
+        elif kind == "store":
+            res = torch.randn(B, cout, T, generator=torch.Generator().manual_seed(3)).to(device)
+            outs[split_w] = ops.conv1d(x, layer, in_slope=0.1, residual=res)
+        else:
+            outs[split_w] = ops.conv1d(x, layer, in_slope=0.1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[True]).all()
+    assert torch.equal(outs[True], outs[False])
 
 
 def test_conv1d_masked_split_accumulate(device):

@@ -44,7 +44,9 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   if (d.epi == VITS_EPI_STORE && d.split < d.m) VITS_CHECK_ARG(d.out1.y != nullptr);
   if ((reinterpret_cast<uintptr_t>(d.w) & 15) != 0) return VITS_E_SHAPE;
   VITS_CHECK_ARG(d.wdtype == VITS_WDT_F32 || d.wdtype == VITS_WDT_BF16 ||
-                 d.wdtype == VITS_WDT_F16 || d.wdtype == VITS_WDT_F32S);
+                 d.wdtype == VITS_WDT_F16 || d.wdtype == VITS_WDT_F32S ||
+                 d.wdtype == VITS_WDT_F32P);
+  if (d.wdtype == VITS_WDT_F32P) VITS_CHECK_SHAPE(d.kc == 16 || d.kc == 32);
   if (d.wdtype != VITS_WDT_F32) VITS_CHECK_SHAPE((d.kc % 16) == 0);
   if (d.gmask) VITS_CHECK_ARG(d.epi == VITS_EPI_STORE && d.split >= d.m);
   if (d.io16) VITS_CHECK_ARG(d.wdtype == VITS_WDT_BF16 || d.wdtype == VITS_WDT_F16);
@@ -67,6 +69,8 @@ int conv1d_group(const vits_conv1d_desc* d, int n, int batch, hipStream_t s) {
       return vits_conv1d_dispatch_f16(g, s);
     case VITS_WDT_F32S:
       return vits_conv1d_dispatch_f32s(g, s);
+    case VITS_WDT_F32P:
+      return vits_conv1d_dispatch_f32p(g, s);
     default:
       return vits_conv1d_dispatch_f32(g, s);
   }

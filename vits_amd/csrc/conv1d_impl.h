@@ -88,10 +88,14 @@ constexpr int VITS_W_TILE_BF = 6144;
 constexpr int VITS_W_TILE_SPL = 11264;
 // ... and with the W chunk pre-split through registers (128x128 tiles)
 constexpr int VITS_W_TILE_WPS = 8192;
+// split fp32 with the weights pre-split on the host (VITS_WDT_F32P): three
+// bf16 planes [cin_pad/16][k][2][3][m_pad][8], the A fragments read straight
+// from global memory (L2) into registers - W never enters LDS
+constexpr int VITS_WDT_F32P_ = VITS_WDT_F32P;
 // low-precision element type of weight type WT (VITS_WDT_BF16 / VITS_WDT_F16)
 template <int WT>
 struct LowP {
-  typedef __bf16 T;
+  typedef __bf16 T;  // (bf16, split fp32 and its pre-split planes)
 };
 template <>
 struct LowP<VITS_WDT_F16> {
@@ -166,7 +170,7 @@ struct ConvGroup {
 // activations in fp16, as the reference's autocast convs return them),
 // half the bytes of the fp32-I/O kernel; accumulation stays fp32.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false>
-__global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
+__global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
   static_assert(!IO16 || WT != VITS_WDT_F32, "IO16 needs a 16-bit operand type");
   const int gi = (int)blockIdx.z / G.batch;
   const vits_conv1d_desc& p = G.d[gi];
@@ -174,7 +178,12 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   constexpr bool BF = WT != VITS_WDT_F32;  // 16-channel slab layout, 16-deep k-steps
   // split fp32: the slab layouts hold fp32 (LDS and W image), split into
   // three bf16 terms in registers per fragment (split3_bf16)
-  constexpr bool SPL = WT == VITS_WDT_F32S;
+  // pre-split weights (VITS_WDT_F32P): the split-fp32 arithmetic with the A
+  // fragments loaded from the host-split bf16 planes in global memory, one
+  // k-step ahead, into registers; LDS holds only the X window, double
+  // buffered (one barrier per chunk); kc == 16, one chunk = one 16-channel slab
+  constexpr bool WG = WT == VITS_WDT_F32P;
+  constexpr bool SPL = WT == VITS_WDT_F32S || WG;
   constexpr int WQ = SPL ? 8 : 4;  // float slots per (W row, 8 channels)
   // split fp32 on 128x128 tiles: the W chunk is staged pre-split as well
   // (three bf16 planes, one buffer; global -> registers under the MFMAs,
@@ -182,7 +191,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   // loop runs no VALU split; kc*k*BM <= VITS_W_TILE_WPS
   // (measured on MI355X: k=3 126 -> 137 TF/s on 128x128; no gain on 64x128,
   // whose 2-tap upsamplers lose 20 %)
-  constexpr bool WPS = SPL && BM == 128 && BN == 128;
+  constexpr bool WPS = SPL && !WG && BM == 128 && BN == 128;
   constexpr int NWU = VITS_W_TILE_WPS / 8 / 256;  // 8-float W entries per thread
   typedef typename LowP<WT>::T lp_t;
   typedef lp_t lpx8 __attribute__((ext_vector_type(8)));
@@ -203,7 +212,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   const int xw = BN + (k - 1) * dil;
   const int xw_pad = (xw + 3) & ~3;
   const int wrows = kc * k;
-  const int wsz = (BF && !SPL) ? wrows * BM / 2 : wrows * BM;  // W stage in float slots
+  const int wsz = WG ? 0 : (BF && !SPL) ? wrows * BM / 2 : wrows * BM;  // W stage in float slots
   // X window geometry.  Scalar staging (any strides): rows of xw_pad
   // elements starting at column xstart.  V4 staging (time-contiguous rows,
   // 16-byte aligned, tin % 4 == 0): 16-byte blocks from the aligned column
@@ -225,8 +234,8 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   // two stages: [W0][X0][W1][X1] (split fp32: [W0][W1][X])
   float* const stage0 = smem;
   float* const stage1 = SPL ? smem + wsz : smem + wsz + xslots;
-  float* const xbuf1 = WPS ? smem + 3 * wsz / 2 : SPL ? smem + 2 * wsz : stage0 + wsz;  // X of stage 0
-  float* const xbuf2 = SPL ? xbuf1 : stage1 + wsz;            // X of stage 1
+  float* const xbuf1 = WG ? smem : WPS ? smem + 3 * wsz / 2 : SPL ? smem + 2 * wsz : stage0 + wsz;  // X of stage 0
+  float* const xbuf2 = WG ? smem + xslots : SPL ? xbuf1 : stage1 + wsz;  // X of stage 1
 
   const int b = (int)blockIdx.z - gi * G.batch;
   const int n0 = blockIdx.x * BN;
@@ -252,7 +261,10 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   const int xstart = n0 - p.pad_left - xsh;  // V4: a multiple of 4
   const float slope = p.in_slope;
   const bool act_in = slope != 1.0f;
-  constexpr int MAXX = XTile<BN, BF, IO16>::regs;
+  // (pre-split W, no W stage in LDS: the 16-bit activations' larger window
+  // budget, i.e. 32-channel chunks on 128-column tiles)
+  constexpr bool XB = IO16 || WG;
+  constexpr int MAXX = XTile<BN, BF, XB>::regs;
   // T4 staging (16-bit activations, V4 rows): a unit is 4 channels x 4 time
   // steps - four 8-byte row loads, transposed in registers into four 8-byte
   // [t][4 channels] pieces, one ds_write_b64 each (the element-wise [t][c]
@@ -260,7 +272,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   // of a 16-lane group cover 4 channel quads x 4 time blocks: their LDS
   // pieces fall on distinct banks for kcp = 4 (mod 16) halves per row.
   constexpr bool T4 = V4 && (IO16 || SPL);
-  constexpr int NU = T4 ? (XTile<BN, BF, IO16>::floats / 16 + 48 + 255) / 256
+  constexpr int NU = T4 ? (XTile<BN, BF, XB>::floats / 16 + 48 + 255) / 256
                         : V4 ? MAXX / 4 : MAXX;  // staging units per thread
   constexpr int UW = V4 ? 4 : 1;            // elements per unit (per row)
   typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -505,6 +517,107 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
   const int nchunks = p.cin_pad / kc;
   const int half = kc >> 1;
   const int steps = k * half;  // MFMA k-steps per chunk
+
+  if constexpr (WG) {
+    // ---- pre-split W from global (VITS_WDT_F32P) ----------------------------
+    // A chunk of kc = 16 G channels is G slabs; its k-steps run slab-major
+    // (g, then tap j), so the flat step s = slab * k + j walks the weight
+    // image contiguously: the A fragments of step s (plane q, row r, half
+    // lhi) are the 16 bytes at
+    //   w + ((s * 2 + lhi) * 3 + q) * m_pad * 8 + r * 8   (bf16 elements),
+    // i.e. 32 consecutive rows = 512 contiguous bytes per load instruction.
+    const int G = kc >> 4;
+    const int nst = G * k;  // k-steps per chunk
+    const int total = nchunks * nst;
+    const __bf16* wbase = reinterpret_cast<const __bf16*>(p.w) +
+                          ((int64_t)(lhi * 3) * p.m_pad + m0 + wm + l32) * 8;
+    const int64_t wstep = (int64_t)48 * p.m_pad;
+    auto loadA = [&](int s, bf16x8_t (*a)[TM]) {
+      const __bf16* wp = wbase + (int64_t)(s < total ? s : total - 1) * wstep;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+          a[q][mi] = *reinterpret_cast<const bf16x8_t*>(wp + ((int64_t)q * p.m_pad + mi * 32) * 8);
+    };
+    // B fragments of tap j, slab g of the chunk: rows wn + ni*32 + l32 + j*dil
+    // of the [t][kcp] window planes, channels 16 g + 8 lhi .. + 8
+    const __bf16* const xlane0 = reinterpret_cast<const __bf16*>(xbuf1) +
+                                 (wn + l32 + xsh) * kcp + 8 * lhi;
+    const int xdelta = (int)(reinterpret_cast<const __bf16*>(xbuf2) -
+                             reinterpret_cast<const __bf16*>(xbuf1));
+    auto loadB = [&](int buf, int j, int g, bf16x8_t* bh, bf16x8_t* bm, bf16x8_t* bl) {
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const lpx4* xp = reinterpret_cast<const lpx4*>(
+            xlane0 + buf * xdelta + (ni * 32 + j * dil) * kcp + 16 * g);
+        const int P4 = xpl / 4;  // plane stride in 8-byte pieces
+        bh[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+        bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    };
+    // the same six products in the same order as the F32S path (bitwise the
+    // same result for kc = 16): small terms first
+    auto mma = [&](bf16x8_t (*a)[TM], const bf16x8_t* bh, const bf16x8_t* bm,
+                   const bf16x8_t* bl) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+          f32x16 c = acc[mi][ni];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bl[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][mi], bh[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bm[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bm[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bh[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bh[ni], c, 0, 0, 0);
+          acc[mi][ni] = c;
+        }
+    };
+    bf16x8_t a0[3][TM], a1[3][TM];
+    bf16x8_t bh0[TN], bm0[TN], bl0[TN], bh1[TN], bm1[TN], bl1[TN];
+    loadA(0, a0);
+    gload(0);
+    lstore(xbuf1, 0);
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const bool more = ch + 1 < nchunks;
+      if (more) gload((ch + 1) * kc);  // in flight under this chunk's MFMAs
+      const int buf = ch & 1;
+      const int s0 = ch * nst;
+      // (j, g) of step st; next() advances it: taps fastest, then slabs
+      int j = 0, g = 0;
+      auto next = [&]() {
+        if (++j == k) {
+          j = 0;
+          ++g;
+        }
+      };
+      loadB(buf, 0, 0, bh0, bm0, bl0);
+      int st = 0;
+      for (; st + 2 <= nst; st += 2) {
+        next();
+        loadA(s0 + st + 1, a1);
+        loadB(buf, j, g, bh1, bm1, bl1);
+        mma(a0, bh0, bm0, bl0);
+        next();
+        loadA(s0 + st + 2, a0);  // (st + 2 == nst: the next chunk's first step)
+        if (st + 2 < nst) loadB(buf, j, g, bh0, bm0, bl0);
+        mma(a1, bh1, bm1, bl1);
+      }
+      if (st < nst) {  // odd step count: the last step, and the next chunk's A
+        loadA(s0 + nst, a1);
+        mma(a0, bh0, bm0, bl0);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi) a0[q][mi] = a1[q][mi];
+      }
+      if (more) lstore(buf ? xbuf1 : xbuf2, (ch + 1) * kc);
+      __syncthreads();
+    }
+  } else {
 
   if constexpr (WPS)
     wgload(0);
@@ -770,6 +883,7 @@ __global__ __launch_bounds__(256, WT == VITS_WDT_F32S ? 2 : 3) void conv1d_mfma_
     }
     __syncthreads();
   }
+  }  // !WG
 
   // ---- epilogue -----------------------------------------------------------
   const int len_b = p.lengths ? p.lengths[b] : 0x7fffffff;
@@ -922,32 +1036,35 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
   int gx = 0, gy = 0;
   for (int i = 0; i < g.n; ++i) {
     const vits_conv1d_desc& d = g.d[i];
-    constexpr bool SPL = WT == VITS_WDT_F32S;
-    const size_t wsz = (BF && !SPL) ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
+    constexpr bool WG = WT == VITS_WDT_F32P;
+    constexpr bool SPL = WT == VITS_WDT_F32S || WG;
+    const size_t wsz = WG ? 0 : (BF && !SPL) ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
     const size_t xsz = (size_t)d.kc * xrs[i];
     if (wsz > (size_t)(SPL ? (BM == 128 && BN == 128 ? VITS_W_TILE_WPS : VITS_W_TILE_SPL)
                            : BF ? VITS_W_TILE_BF : VITS_W_TILE) ||
-        xsz > (size_t)XTile<BN, BF, IO16>::floats)
+        xsz > (size_t)XTile<BN, BF, IO16 || WG>::floats)
       return VITS_E_UNSUP;
+    if (WG && d.kc != 16 && d.kc != 32) return VITS_E_UNSUP;
     // 32-bit window offsets
     if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
       return VITS_E_UNSUP;
     if (V4 && (IO16 || SPL)) {  // T4 staging: kc/4 channel quads x ceil(nb/4)*4 blocks
-      constexpr int nu = (XTile<BN, BF, IO16>::floats / 16 + 48 + 255) / 256;
+      constexpr int nu = (XTile<BN, BF, IO16 || WG>::floats / 16 + 48 + 255) / 256;
       if (d.kc % 16 || (size_t)d.kc * ((xrs[i] / 4 + 3) / 4) > (size_t)nu * 256)
         return VITS_E_UNSUP;
     }
     const size_t xslots = BF ? (SPL ? (3 * xrs[i] * (d.kc + 4) + 1) / 2 : (xrs[i] * (d.kc + 4) + 1) / 2) : xsz;
     // + tail pad: the software pipeline reads one k-step past the last chunk
     // (split fp32: one X buffer)
-    const size_t wst = (SPL && BM == 128 && BN == 128) ? 3 * wsz / 2 : 2 * wsz;  // W stage(s)
+    const size_t wst = WG ? 0 : (SPL && BM == 128 && BN == 128) ? 3 * wsz / 2 : 2 * wsz;  // W stage(s)
     // split fp32 ([W0][W1][X] / [W][X]): a W read-ahead lands in the next W
     // stage or in X; only the B read-ahead of the last plane runs past the
     // end, by < (dil + 2) window rows of kc + 4 bf16 - a tail that keeps the
     // k=7, d=5 64x128 tile at two workgroups per CU
     const size_t tail = SPL ? (size_t)(d.dil + 2) * (d.kc + 4) / 2 + 64
                             : 2 * (size_t)d.k * BM + 2 * xrs[i] + 64;
-    const size_t l = sizeof(float) * (wst + (SPL ? 1 : 2) * xslots + tail);
+    // (WG: two X buffers, no W)
+    const size_t l = sizeof(float) * (wst + ((SPL && !WG) ? 1 : 2) * xslots + tail);
     if (l > lds) lds = l;
     const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;
     if (x > gx) gx = x;
@@ -997,12 +1114,14 @@ int launch_tile(const ConvGroup& g, hipStream_t s) {
                     (d.tin & 3) == 0 && d.pad_left >= 0 &&
                     (reinterpret_cast<uintptr_t>(d.x) & align) == 0 &&
                     (size_t)d.kc * xrs4[i] <=
-                        (size_t)(d.io16 ? XTile<BN, BF, true>::floats : XTile<BN, BF>::floats);
+                        (size_t)((d.io16 || WT == VITS_WDT_F32P) ? XTile<BN, BF, true>::floats
+                                                                  : XTile<BN, BF>::floats);
     nv4 += v4;
     nio += d.io16 != 0;
   }
-  if (nio != 0 && (nio != g.n || !BF || WT == VITS_WDT_F32S)) return VITS_E_UNSUP;
-  if constexpr (BF && WT != VITS_WDT_F32S) {  // (split fp32 has fp32 I/O only)
+  if (nio != 0 && (nio != g.n || !BF || WT == VITS_WDT_F32S || WT == VITS_WDT_F32P))
+    return VITS_E_UNSUP;
+  if constexpr (BF && WT != VITS_WDT_F32S && WT != VITS_WDT_F32P) {  // (split: fp32 I/O only)
     if (nio) {
       if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, true>(g, s, xrs4);
       if (nv4 != 0) return VITS_E_UNSUP;
@@ -1044,11 +1163,12 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
       bool fits128 = true;
       for (int i = 0; i < g.n; ++i) {
         const int xw_pad128 = (128 + (g.d[i].k - 1) * g.d[i].dil + 3) & ~3;
-        fits128 = fits128 && g.d[i].kc * xw_pad128 <= (g.d[i].io16 ? XTile<128, BF, true>::floats
-                                                                    : XTile<128, BF>::floats);
+        fits128 = fits128 && g.d[i].kc * xw_pad128 <= ((g.d[i].io16 || WT == VITS_WDT_F32P)
+                                                          ? XTile<128, BF, true>::floats
+                                                          : XTile<128, BF>::floats);
       }
       if (blocks < 512 && fits128) return launch_tile<64, 128, 2, 2, WT>(g, s);
-      if constexpr (WT == VITS_WDT_F32S) {
+      if constexpr (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) {
         // split fp32: 2x2 waves (32x128 per wave) - each A-fragment split
         // feeds four B fragments instead of two (k=11 convs +1..3 %)
         return launch_tile<64, 256, 2, 2, WT>(g, s);
@@ -1069,3 +1189,4 @@ int vits_conv1d_dispatch_f32(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_bf16(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_f16(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_f32s(const vits_conv::ConvGroup& g, hipStream_t s);
+int vits_conv1d_dispatch_f32p(const vits_conv::ConvGroup& g, hipStream_t s);

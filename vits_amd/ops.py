@@ -17,7 +17,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, WDT_F32S, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
+from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, WDT_F32P, WDT_F32S, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
                    ResblockPairDesc,
                    EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS,
                    check)
@@ -168,6 +168,8 @@ class PackedConv:
 
     @property
     def m_pad(self) -> int:
+        if self.wdtype == WDT_F32P:
+            return self.w.shape[4]
         return self.w.shape[3] if self.wdtype != WDT_F32 else self.w.shape[2]
 
     @property
@@ -225,6 +227,50 @@ def _pick_tile_f32s(m: int, k: int) -> int:
     return TILE_64x256
 
 
+def _pick_tile_f32p(m: int, k: int) -> int:
+    """Tile of the pre-split-weight kernel (VITS_WDT_F32P): W is read from
+    global memory, so the LDS holds only the double-buffered window and
+    128x128 (2x2 waves of 64x64: two A and two B fragment triples feed 24
+    MFMAs per k-step) fits every decoder shape; grids too small to fill the
+    chip twice fall back to 64x128 in the dispatcher."""
+    return TILE_128x128 if m >= 128 else TILE_64x128
+
+
+# channels per K-chunk of the pre-split kernel: 32 (two slabs, half the
+# chunk barriers) when the window of a 32-channel chunk fits the staging
+# budget (conv1d_impl.h XTile<BN, true, true>: 6144 / 10240 elements for 128
+# / 256 columns), else 16; VITS_F32P_KC=16 forces single slabs
+F32P_MAX_KC = int(os.environ.get("VITS_F32P_KC", "32"))
+
+
+def _kc_f32p(cin_pad: int, k: int, dil: int, tile: int) -> int:
+    bn = TILE_COLS[tile]
+    xrs = (bn + (k - 1) * dil + 3 + 3) // 4 * 4  # window row incl. the 16-byte alignment shift
+    budget = 6144 if bn <= 128 else 10240
+    if F32P_MAX_KC >= 32 and cin_pad % 32 == 0 and 32 * xrs <= budget:
+        return 32
+    return 16
+
+
+# pre-split weights for split fp32 (VITS_SPLIT_W=0: the F32S kernel, which
+# splits the fp32 weight slabs per fragment in registers)
+SPLIT_W = os.environ.get("VITS_SPLIT_W", "1") != "0"
+
+
+def split_planes(w: torch.Tensor) -> torch.Tensor:
+    """Exact three-term bf16 split of an fp32 tensor, stacked on a new
+    dimension -4 as (hi, mid, lo) planes: hi = x truncated to bf16, mid =
+    (x - hi) truncated, lo = x - hi - mid (<= 8 significant bits), so
+    hi + mid + lo == x bit for bit - conv1d_impl.h split3_bf16 on the host."""
+    w = w.to(torch.float32).contiguous()
+    mask = torch.tensor(-65536, dtype=torch.int32, device=w.device)
+    h = (w.view(torch.int32) & mask).view(torch.float32)
+    r = w - h
+    m = (r.view(torch.int32) & mask).view(torch.float32)
+    lo = r - m
+    return torch.stack([h, m, lo], dim=-3).to(torch.bfloat16)
+
+
 # Split-fp32 layers need >= this many GEMM rows: the sweep above measured it
 # ahead of the exact-f32 kernel on every 128- / 256-channel decoder conv
 # (+8..35 %), the upsamplers, conv_pre and the flow, but behind it on the
@@ -251,6 +297,14 @@ def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
         w = w32.new_zeros(cin_pad, k, m_pad)
         w[:layer.cin] = w32
         w = w.view(cin_pad // kc, kc // 8, 8, k, m_pad).permute(0, 3, 1, 4, 2).contiguous()
+        if SPLIT_W:
+            # [cin_pad/16][k][2][3][m_pad][8] bf16: planes next to the lane half
+            tile = _pick_tile_f32p(layer.m, layer.k)
+            return PackedConv(split_planes(w), layer.bias, layer.cin, layer.m, layer.k,
+                              layer.dil, layer.pad_left, layer.epi, tile,
+                              _kc_f32p(cin_pad, layer.k, layer.dil, tile), up_u=layer.up_u,
+                              up_pad=layer.up_pad, out_channels=layer.out_channels,
+                              extra=layer.extra, wdtype=WDT_F32P)
         return PackedConv(w, layer.bias, layer.cin, layer.m, layer.k, layer.dil,
                           layer.pad_left, layer.epi, _pick_tile_f32s(layer.m, layer.k), kc,
                           up_u=layer.up_u, up_pad=layer.up_pad,
@@ -416,7 +470,8 @@ def conv_flops(desc: ConvDesc, batch: int) -> int:
 # PF/s; split fp32 = six bf16 MFMAs per fp32 product, 2.5 PF / 6.
 BF16_DENSE_PEAK_TFLOPS = 2500.0
 MFMA_PEAK_TFLOPS = {WDT_F32: 157.3, WDT_BF16: BF16_DENSE_PEAK_TFLOPS,
-                    WDT_F16: BF16_DENSE_PEAK_TFLOPS, WDT_F32S: BF16_DENSE_PEAK_TFLOPS / 6}
+                    WDT_F16: BF16_DENSE_PEAK_TFLOPS, WDT_F32S: BF16_DENSE_PEAK_TFLOPS / 6,
+                    WDT_F32P: BF16_DENSE_PEAK_TFLOPS / 6}
 
 
 class ConvTimer:
