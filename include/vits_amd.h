@@ -140,7 +140,12 @@ typedef struct vits_conv1d_desc {
   /* tensors of the 16-bit operand type (strides in elements); fp32 I/O    */
   /* otherwise.  The fp16-autocast training convs keep fp16 activations.   */
   int32_t io16;
-  int32_t reserved;
+  /* with lengths: > 0 = workgroups whose first output position is at or    */
+  /* past lengths[b] + len_skip exit without computing or writing (the      */
+  /* bucketed whole-utterance infer: work follows the utterance, not the     */
+  /* bucket; consumers never read past lengths[b] + halo, halo < len_skip,  */
+  /* and [lengths[b], lengths[b] + len_skip) is written as zeros); 0 = off  */
+  int32_t len_skip;
 } vits_conv1d_desc;
 
 #define VITS_WDT_F32 0
@@ -188,6 +193,28 @@ int vits_expand_prior(const float* attn, const float* m, const float* s, const f
 /* Generator tail: y[b][t] = tanh(sum_{c,j} w[c][j] lrelu(x[b][c][t-3+j], 0.01)) */
 /* w: [channels][7] (conv_post, no bias)                                  */
 /* ---------------------------------------------------------------------- */
+/* ---------------------------------------------------------------------- */
+/* durations -> lengths + expanded prior, on the device (replaces the       */
+/* w = exp(logw)*rate -> ceil -> y_len .item() -> infer_path -> attn @ m /  */
+/* attn @ s -> z_p sequence of models.py:544-553, infer.py:169-176 and     */
+/* commons.py:143-155 without a host sync, over a static bucket t_y):       */
+/*   w_ceil[x] = ceil(exp(logw[b][x]) * rate) (x < x_len[b], else 0;        */
+/*   half_round: fp16 roundings of the half model), y_len = max(sum, 1),   */
+/*   z[b][c][t] = m[b][c][x(t)] + noise(c,t) * s[b][c][x(t)] * noise_scale  */
+/*   for t < y_len (x(t): cum[x-1] <= t < cum[x]), 0 for y_len <= t < t_y;  */
+/*   lens[i][b] = y_len * stage_mult[i].  noise_mode 0: noise [B][C][t_y];  */
+/*   1: element (c, t) at noise[s + c*y_len + t], s = noise_start[b] mod    */
+/*   (noise_len - C*y_len) (EmoVITS's buffer slice at a random start,      */
+/*   infer.py:172-175).  t_x <= 4096, n_stage <= 8.                         */
+/* ---------------------------------------------------------------------- */
+int vits_expand_durations(const float* logw, int64_t logw_bstride, const int32_t* x_len, int t_x,
+                          float rate, int half_round, const float* m, const float* s,
+                          int64_t ms_bstride, int32_t ms_cstride, const float* noise,
+                          int noise_mode, const int32_t* noise_start, int64_t noise_len,
+                          float noise_scale, float* z,
+                          int batch, int channels, int t_y, int32_t* lens,
+                          const int32_t* stage_mult, int n_stage, void* stream);
+
 int vits_conv_post_tanh(const float* x, int64_t x_bstride, int32_t x_cstride, const float* w,
                         float* y, int batch, int channels, int t_len, int ksize, void* stream);
 
@@ -429,7 +456,10 @@ typedef struct vits_resblock_pair_desc {
   int32_t y_cstride;
   int32_t accumulate;
   float post_div;
-  int32_t reserved;
+  int32_t len_skip;      /* as vits_conv1d_desc.len_skip                     */
+  /* [B] valid lengths or NULL: the gated tensor is zero and the output 0  */
+  /* at t >= lengths[b] (the utterance ends there, as the convs' masks)    */
+  const int32_t* lengths;
 } vits_resblock_pair_desc;
 int vits_resblock_pair_forward(const vits_resblock_pair_desc* d, int n, int batch, void* stream);
 int vits_resblock_pair_kc(int channels, int k, int dil, int* kc1, int* kc2);

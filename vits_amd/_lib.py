@@ -80,7 +80,7 @@ class ConvDesc(C.Structure):
         ("gmask_cstride", C.c_int32),
         ("gmask_slope", C.c_float),
         ("io16", C.c_int32),
-        ("reserved", C.c_int32),
+        ("len_skip", C.c_int32),
     ]
 
 
@@ -112,7 +112,8 @@ class ResblockPairDesc(C.Structure):
         ("y_cstride", C.c_int32),
         ("accumulate", C.c_int32),
         ("post_div", C.c_float),
-        ("reserved", C.c_int32),
+        ("len_skip", C.c_int32),
+        ("lengths", C.c_void_p),
     ]
 
 
@@ -220,6 +221,12 @@ _SIGS = {
     "vits_expand_prior": (
         C.c_int,
         [C.c_void_p] * 5 + [C.c_int] * 5 + [C.c_float, C.c_void_p],
+    ),
+    "vits_expand_durations": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p,
+         C.c_int64, C.c_int32, C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_float, C.c_void_p,
+         C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p],
     ),
     "vits_conv_post_tanh": (
         C.c_int,

@@ -8,6 +8,9 @@
 //                         models.py:37-38,49-52 (DurationPredictor.cond1/2)
 //   vits_expand_prior     attn-weighted prior expansion + reparameterised
 //                         noise, models.py:569-571 (infer_p2)
+//   vits_expand_durations durations -> lengths + expanded prior on the device
+//                         (models.py:544-553, commons.py:143-155), the
+//                         host sync of infer() removed
 //   vits_conv_post_tanh   Generator tail, models.py:315-317
 #include "common.h"
 
@@ -124,6 +127,124 @@ __global__ __launch_bounds__(256) void expand_prior_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
+// durations -> lengths + expanded prior on the device (no host sync).
+// models.py:544-553 / infer.py:169-176 / commons.py:143-155 compute
+//   w = exp(logw) * rate; w_ceil = ceil(w); y_len = max(sum(w_ceil), 1)
+//   (.item(): the host sync), path = infer_path(w_ceil), z = path-expanded
+//   m + noise * path-expanded s (* noise_scale)
+// here every frame of a static bucket t_y finds its token by binary search
+// in the cumulative durations (frame t belongs to token x iff cum[x-1] <= t
+// < cum[x], the one-hot of infer_path) and frames t >= y_len are zero; the
+// per-stage lengths y_len * mult[i] (the masks of the flow / decoder convs)
+// go to lens[i][b].  Workgroup = (64 frames, utterance); every workgroup
+// rescans its utterance's durations (t_x <= 4096) in LDS.
+// ---------------------------------------------------------------------------
+constexpr int ED_T = 64;
+constexpr int ED_MAX_TX = 4096;
+constexpr int ED_MAX_STAGES = 8;
+struct EdStages {
+  int32_t mult[ED_MAX_STAGES];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void expand_durations_kernel(
+    const float* __restrict__ logw, int64_t logw_bstride, const int32_t* __restrict__ x_len,
+    int t_x, float rate, int half_round, const float* __restrict__ m, const float* __restrict__ s,
+    int64_t ms_bstride, int ms_cstride, const float* __restrict__ noise, int noise_mode,
+    const int32_t* __restrict__ noise_start, int64_t noise_len, float noise_scale,
+    float* __restrict__ z, int channels, int t_y, int batch, int32_t* __restrict__ lens,
+    const EdStages st) {
+  __shared__ int cum[ED_MAX_TX];
+  __shared__ int part[256];
+  __shared__ int xi[ED_T];
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int nx = x_len ? min(x_len[b], t_x) : t_x;
+  // 1) integer durations of this thread's consecutive tokens, block scan
+  const int per = (t_x + 255) / 256;
+  const int xb0 = tid * per;
+  int local = 0;
+  for (int i = 0; i < per; ++i) {
+    const int x = xb0 + i;
+    if (x < t_x) {
+      int d = 0;
+      if (x < nx) {
+        float w = expf(logw[(int64_t)b * logw_bstride + x]);
+        if (half_round) w = (float)(_Float16)w;  // the fp16 model's torch.exp
+        w = w * rate;
+        if (half_round) w = (float)(_Float16)w;
+        d = (int)ceilf(w);
+      }
+      local += d;
+      cum[x] = local;  // inclusive within the thread for now
+    }
+  }
+  part[tid] = local;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int v = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  const int base = tid > 0 ? part[tid - 1] : 0;
+  for (int i = 0; i < per; ++i) {
+    const int x = xb0 + i;
+    if (x < t_x) cum[x] += base;
+  }
+  __syncthreads();
+  // y_len = clamp_min(sum(w_ceil), 1): the half model sums in fp16 (its
+  // torch.sum result rounds to half: totals > 2048 frames round to even)
+  int y_len = part[255];
+  if (half_round) y_len = (int)(float)(_Float16)(float)y_len;
+  y_len = max(y_len, 1);
+  const int total = part[255];
+  if (blockIdx.x == 0 && tid < st.n) lens[tid * batch + b] = y_len * st.mult[tid];
+  // 2) token of each frame of this workgroup: first x with cum[x] > t
+  const int t0 = blockIdx.x * ED_T;
+  if (tid < ED_T) {
+    const int t = t0 + tid;
+    int r = -1;
+    if (t < y_len && t < t_y && t < total) {  // (frames past the durations: no token)
+      int lo = 0, hi = t_x - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cum[mid] > t) hi = mid; else lo = mid + 1;
+      }
+      r = lo;
+    }
+    xi[tid] = r;
+  }
+  __syncthreads();
+  // 3) z[b][c][t] = m[c][x] + (noise(c, t) * s[c][x]) * noise_scale, 0 past y_len
+  const float* mb = m + (int64_t)b * ms_bstride;
+  const float* sb = s + (int64_t)b * ms_bstride;
+  // mode 1: the slice start (infer.py:173 draws randint(len - C*y_len)); a
+  // raw draw is folded into [0, noise_len - C*y_len) here, where y_len is known
+  int64_t nbase = 0;
+  if (noise_mode) {
+    const int64_t room = noise_len - (int64_t)channels * y_len;
+    nbase = noise_start ? (int64_t)noise_start[b] % (room > 1 ? room : 1) : 0;
+  }
+  for (int i = tid; i < channels * ED_T; i += 256) {
+    const int c = i / ED_T;
+    const int tl = i - c * ED_T;
+    const int t = t0 + tl;
+    if (t >= t_y) continue;
+    const int x = xi[tl];
+    float v = 0.f;
+    if (x >= 0) {
+      // mode 0: noise [B][C][t_y]; mode 1: EmoVITS's buffer slice viewed as
+      // [C][y_len] from element noise_start[b] (infer.py:172-175)
+      const float n = noise_mode ? noise[nbase + (int64_t)c * y_len + t]
+                                 : noise[((int64_t)b * channels + c) * t_y + t];
+      v = mb[(int64_t)c * ms_cstride + x] + (n * sb[(int64_t)c * ms_cstride + x]) * noise_scale;
+    }
+    z[((int64_t)b * channels + c) * t_y + t] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generator tail: one thread per output sample; the input window of the
 // workgroup ([channels][256 + k - 1]) is staged in LDS with the 0.01 leaky
 // relu applied once per element.
@@ -207,6 +328,29 @@ extern "C" int vits_expand_prior(const float* attn, const float* m, const float*
   dim3 grid((t_y + EP_T - 1) / EP_T, batch);
   hipLaunchKernelGGL(expand_prior_kernel, grid, dim3(256), lds, as_stream(stream), attn, m, s,
                      noise, z, channels, t_y, t_x, exp_s, noise_scale);
+  return vits_launch_status();
+}
+
+extern "C" int vits_expand_durations(const float* logw, int64_t logw_bstride,
+                                     const int32_t* x_len, int t_x, float rate, int half_round,
+                                     const float* m, const float* s, int64_t ms_bstride,
+                                     int32_t ms_cstride, const float* noise, int noise_mode,
+                                     const int32_t* noise_start, int64_t noise_len,
+                                     float noise_scale, float* z,
+                                     int batch, int channels, int t_y, int32_t* lens,
+                                     const int32_t* stage_mult, int n_stage, void* stream) {
+  VITS_CHECK_ARG(logw && m && s && noise && z && lens && batch > 0 && channels > 0 && t_y > 0 &&
+                 t_x > 0);
+  VITS_CHECK_ARG(n_stage >= 1 && n_stage <= ED_MAX_STAGES && (n_stage == 1 || stage_mult));
+  VITS_CHECK_SHAPE(t_x <= ED_MAX_TX && ms_cstride >= t_x);
+  EdStages st;
+  st.n = n_stage;
+  for (int i = 0; i < ED_MAX_STAGES; ++i) st.mult[i] = i < n_stage ? (stage_mult ? stage_mult[i] : 1) : 0;
+  dim3 grid((t_y + ED_T - 1) / ED_T, batch);
+  hipLaunchKernelGGL(expand_durations_kernel, grid, dim3(256), 0, as_stream(stream), logw,
+                     logw_bstride, x_len, t_x, rate, half_round, m, s, ms_bstride, ms_cstride,
+                     noise, noise_mode, noise_start, noise_len, noise_scale, z, channels, t_y,
+                     batch, lens, st);
   return vits_launch_status();
 }
 

@@ -80,11 +80,16 @@ __global__ __launch_bounds__(256, 2) void resblock_pair_kernel(const RbGroup G) 
   const int k = p.k;
   const int dil = p.dil;
   const int T = p.t_len;
+  // valid length of this utterance (masked decoder of the bucketed infer):
+  // the gated tensor is zero past it (c2's zero padding at the utterance
+  // end) and the outputs there are 0, as the conv kernel's lengths mask
+  const int L = p.lengths ? min(T, (int)p.lengths[b]) : T;
   const int p1 = (k - 1) * dil / 2;
   const int p2 = (k - 1) / 2;
   const int BN = NG - 2 * p2;
   const int n0 = blockIdx.x * BN;
   if (n0 >= T) return;
+  if (p.lengths && p.len_skip > 0 && n0 >= L + p.len_skip) return;  // bucketed infer
 
   extern __shared__ float smem[];
   float* const erow = smem;                 // [2M]: phase-1 / phase-2 row constants
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(256, 2) void resblock_pair_kernel(const RbGroup G) 
     for (int ni = 0; ni < TN; ++ni) {
       const int col = wn + ni * 32 + l32;
       const int t = n0 - p2 + col;
-      const bool in = t >= 0 && t < T;
+      const bool in = t >= 0 && t < L;
       const int rloc = wm + mi * 32 + 4 * lhi;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
@@ -346,6 +351,7 @@ __global__ __launch_bounds__(256, 2) void resblock_pair_kernel(const RbGroup G) 
         for (int r = 0; r < 16; ++r) {
           float o = v[r];
           if (p.post_div != 1.0f) o = o / p.post_div;
+          if (t >= L) o = 0.f;
           yb[(int64_t)(rloc + (r & 3) + 8 * (r >> 2)) * p.y_cstride + t] = o;
         }
       }

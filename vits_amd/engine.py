@@ -165,23 +165,30 @@ class GeneratorPlan:
         return ops.linear_rows(g, self.cond_w, self.cond_b)
 
     def run(self, x: torch.Tensor, g: torch.Tensor, cond: Optional[torch.Tensor] = None,
-            out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """x [B, C_in, T] fp32 -> wav [B, 1, T * prod(u)]."""
+            out: Optional[torch.Tensor] = None,
+            lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x [B, C_in, T] fp32 -> wav [B, 1, T * prod(u)].  ``lengths``
+        (int32 [1 + n_stages, B], device): utterance b ends at lengths[0][b]
+        frames (conv_pre) and lengths[i + 1][b] samples after upsampler i -
+        every conv output is zero past it, so each utterance sees the zero
+        padding of its own end, exactly as the reference's unmasked decoder
+        on that many frames (models.py:306-318)."""
         B = x.shape[0]
         if cond is None:
             cond = self.conds(g)
         dev = x.device
-        h = ops.conv1d(x, self.conv_pre)
-        for up, blocks in zip(self.ups, self.stages):
-            xu = ops.conv1d(h, up, in_slope=0.1)
+        L = (lambda i: None) if lengths is None else (lambda i: lengths[i])
+        h = ops.conv1d(x, self.conv_pre, lengths=L(0))
+        for i, (up, blocks) in enumerate(zip(self.ups, self.stages)):
+            xu = ops.conv1d(h, up, in_slope=0.1, lengths=L(i + 1))
             C, T = xu.shape[1], xu.shape[2]
             xs = torch.empty(B, C, T, device=dev, dtype=torch.float32)
-            self._run_stage(blocks, xu, xs, cond, B, dev)
+            self._run_stage(blocks, xu, xs, cond, B, dev, L(i + 1))
             h = xs
         return ops.conv_post_tanh(h, self.post_w, out=out)
 
     @staticmethod
-    def _run_stage(blocks, xu, xs, cond, B, dev):
+    def _run_stage(blocks, xu, xs, cond, B, dev, lengths=None):
         """The nk ResBlock2 branches of one stage (models.py:311-313) on xu,
         their mean into xs.  Branches are independent until the mean: each
         keeps its own buffers, and the work of one dilation index of all
@@ -204,7 +211,7 @@ class GeneratorPlan:
 
         def c1_desc(j, p):
             return make_desc(blocks[j][p][0], cur[j], make_out(gbuf[j]), in_slope=0.1, cond=cond,
-                             cond_offset=blocks[j][p][2])
+                             cond_offset=blocks[j][p][2], lengths=lengths)
 
         def grouped(ds):
             return [tuple(ds)] if _GROUP_BRANCHES else list(ds)
@@ -217,12 +224,14 @@ class GeneratorPlan:
                 if fj:
                     ops.resblock_pair_launch(tuple(
                         ops.resblock_pair_desc(blocks[j][p][0], blocks[j][p][1], cur[j], dst[j],
-                                               cond=cond, cond_offset=blocks[j][p][2])
+                                               cond=cond, cond_offset=blocks[j][p][2],
+                                               lengths=lengths)
                         for j in fj), B, dev)
                 if cj:
                     descs = grouped(c1_desc(j, p) for j in cj)
                     descs += grouped(make_desc(blocks[j][p][1], gbuf[j],
-                                               make_out(dst[j], res=cur[j])) for j in cj)
+                                               make_out(dst[j], res=cur[j]), lengths=lengths)
+                                     for j in cj)
                     ops.conv1d_launch_seq(descs, B, dev)
                 cur = dst
                 continue
@@ -235,10 +244,11 @@ class GeneratorPlan:
                 if fused[j][p]:
                     ops.resblock_pair_launch(ops.resblock_pair_desc(
                         blocks[j][p][0], blocks[j][p][1], cur[j], xs, cond=cond,
-                        cond_offset=blocks[j][p][2], **kw), B, dev)
+                        cond_offset=blocks[j][p][2], lengths=lengths, **kw), B, dev)
                 else:
                     ops.conv1d_launch_seq([make_desc(blocks[j][p][1], gbuf[j],
-                                                     make_out(xs, res=cur[j], **kw))], B, dev)
+                                                     make_out(xs, res=cur[j], **kw),
+                                                     lengths=lengths)], B, dev)
 
 
 # ---------------------------------------------------------------------------
@@ -397,9 +407,19 @@ class TextEncoderPlan:
         return gen_sin_table(T, self.hidden)[0].to(dev).contiguous()
 
     def run(self, x: torch.Tensor, emo: torch.Tensor, g: torch.Tensor,
-            lengths: Optional[torch.Tensor] = None, exp_logs: bool = False):
+            lengths: Optional[torch.Tensor] = None, exp_logs: bool = False,
+            pad_exact: bool = False):
         """x [B, T, text_channels] (time-major, as the reference takes it).
-        Returns (h [B,H,T], m [B,C,T], logs_or_s [B,C,T])."""
+        Returns (h [B,H,T], m [B,C,T], logs_or_s [B,C,T]).
+
+        lengths: TextEncoder.forward's masking (models.py:167-178,
+        attentions.py:34-46: keys masked, FFN2's conv_2 input masked, but its
+        conv_1 reads the unmasked post-LN activations of padded positions).
+        pad_exact (with lengths): every LayerNorm output is zeroed past the
+        length as well, so each utterance computes exactly what
+        TextEncoder.infer computes on its unpadded tokens (models.py:180-189:
+        the convs see zero padding at the utterance end) - the padded-text
+        buckets of SynthesizerTrn.infer_bucketed."""
         x = _f32(x)
         B, T, _ = x.shape
         dev = x.device
@@ -423,7 +443,8 @@ class TextEncoderPlan:
             _attention_into(qkv, Hc, self.n_heads, lengths, att)
             ops.conv1d_launch(make_desc(L["o"], att, make_out(y)), B, dev)
             g1, b1, e1 = L["n1"]
-            ops.layer_norm_channels(h, g1, b1, e1, residual=y, out=h)
+            ops.layer_norm_channels(h, g1, b1, e1, residual=y, out=h,
+                                    lengths=lengths if pad_exact else None)
             gb = torch.empty(B, L["filt"], T, device=dev, dtype=torch.float32)
             ops.conv1d_launch(make_desc(L["ffn1"], h, make_out(gb), cond=cond,
                                         cond_offset=L["cond_off"], lengths=lengths), B, dev)
@@ -432,7 +453,7 @@ class TextEncoderPlan:
             # Encoder.forward ends with x * x_mask (attentions.py:46): the last
             # LayerNorm zeroes t >= length in its epilogue
             ops.layer_norm_channels(h, g2, b2, e2, residual=y, out=h,
-                                    lengths=lengths if last else None)
+                                    lengths=lengths if (last or pad_exact) else None)
         Cc = self.out_channels
         m = torch.empty(B, Cc, T, device=dev, dtype=torch.float32)
         s = torch.empty_like(m)

@@ -23,10 +23,20 @@ from .export import load_model
 
 class EmoVITS(object):
     def __init__(self, checkpoint_path=None, device=None, *, loglv=0, hps=None, model=None,
-                 graph_cache=0):
+                 graph_cache=0, graph=True, max_graphs=16):
+        """graph: synthesise each utterance as ONE hipGraph replay
+        (SynthesizerTrn.capture_infer_bucketed: the durations, the output
+        length and the path computed on the device, no host sync before the
+        waveform copy), graphs cached per (text bucket, frame bucket), at
+        most ``max_graphs``; graph=False: the reference's eager sequence
+        (infer_p1 -> host durations -> infer_p2)."""
         self.loglv = loglv
         self.graph_cache = int(graph_cache)
         self._p1_graphs = {}
+        self.graph = bool(graph)
+        self.max_graphs = int(max_graphs)
+        self._graphs = {}
+        self._ty_bucket = {}
         if checkpoint_path is None and model is None:
             checkpoint_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "checkpoint",
                                            "checkpoint.pth")
@@ -57,6 +67,8 @@ class EmoVITS(object):
         self.model = model.half().eval().to(self.device)
         self.noise = (torch.randn(1 * self.inter_channels * 4096) * self.noise_scale).half().to(self.device)
         self.inference = self.infer
+        if self.device.type != "cuda":
+            self.graph = False
 
     # -- speaker / emotion banks (infer.py:77-133) ----------------------------
     def _load_spkid_mapping(self, mapfn):
@@ -146,6 +158,8 @@ class EmoVITS(object):
         text_t = torch.from_numpy(np.ascontiguousarray(text)).half().to(self.device).unsqueeze(0)
         emo = emo.to(self.device)
 
+        if self.graph and x_length <= 4096:
+            return self._infer_graph(text_t, emo, sid, duration_rate), emo
         m_p, s_p, logw, g = self._infer_p1(text_t, emo, sid)
         w = torch.exp(logw) * duration_rate
         w_ceil = torch.ceil(w)
@@ -156,6 +170,39 @@ class EmoVITS(object):
         attn = infer_path(w_ceil.float(), x_length, y_length).half()
         wav = self.model.infer_p2(attn, m_p, s_p, g, noise)
         return wav.float().view(-1).cpu().numpy(), emo
+
+
+    # text tokens are padded to a multiple of TX_BUCKET (masked encoder);
+    # frame buckets are powers of two from 256 up to the noise buffer's 4096
+    TX_BUCKET = 32
+
+    def _infer_graph(self, text_t, emo, sid, duration_rate):
+        """One replay of the whole-utterance graph; the one host sync is the
+        waveform copy (y_len read with it).  A bucket that turns out too
+        small (y_len > frames) is re-run once at a large enough bucket,
+        which this text bucket keeps from then on."""
+        t_x = text_t.shape[1]
+        xb = -(-t_x // self.TX_BUCKET) * self.TX_BUCKET
+        while True:
+            tyb = self._ty_bucket.get((xb, duration_rate), 256)
+            key = (xb, tyb, float(duration_rate))
+            run = self._graphs.pop(key, None)
+            if run is None:
+                while len(self._graphs) >= self.max_graphs:
+                    self._graphs.pop(next(iter(self._graphs)))
+                run = self.model.capture_infer_bucketed(
+                    xb, tyb, noise_len=self.noise.numel(), padded_text=True,
+                    length_scale=duration_rate)
+                run.static["noise"].copy_(self.noise.float())
+            self._graphs[key] = run  # most recently used last
+            start = np.random.randint(2 ** 31 - 1)  # folded into range on the device
+            wav, y_len = run(text_t, emo, sid, noise_start=start, x_length=t_x)
+            n = int(y_len[0])  # (synchronises: the copy below needs it anyway)
+            if n <= tyb:
+                return wav[0, 0, :n * self.hop_size].float().cpu().numpy()
+            if tyb >= 4096:
+                raise RuntimeError(f"utterance of {n} frames exceeds the 4096-frame noise buffer")
+            self._ty_bucket[(xb, duration_rate)] = min(4096, 1 << (n - 1).bit_length())
 
 
 def main(argv=None):

@@ -130,11 +130,13 @@ class TextEncoder(nn.Module):
         return h.to(x.dtype), m.to(x.dtype), logs.to(x.dtype)
 
     @torch.no_grad()
-    def forward_masked_hip(self, x, x_lengths, emo, g, exp_logs=False):
-        """Masked TextEncoder.forward on the HIP path (used by ``inference``)."""
+    def forward_masked_hip(self, x, x_lengths, emo, g, exp_logs=False, pad_exact=False):
+        """Masked TextEncoder.forward on the HIP path (used by ``inference``);
+        pad_exact: TextEncoder.infer of each unpadded utterance instead
+        (engine.TextEncoderPlan.run)."""
         plan = engine.get_plan(self, engine.TextEncoderPlan)
         lengths = x_lengths.to(device=x.device, dtype=torch.int32).contiguous()
-        return plan.run(x, emo, g, lengths=lengths, exp_logs=exp_logs)
+        return plan.run(x, emo, g, lengths=lengths, exp_logs=exp_logs, pad_exact=pad_exact)
 
 
 class ResidualCouplingBlock(nn.Module):
@@ -457,6 +459,115 @@ class SynthesizerTrn(nn.Module):
         gplan = engine.get_plan(self.dec, engine.GeneratorPlan)
         o = gplan.run(z, gf)
         return o.to(m_p.dtype)
+
+    # stage multipliers of the lengths the bucketed infer hands to the flow,
+    # conv_pre and the upsample stages (frames -> samples after each ups)
+    def _stage_mult(self):
+        mult, u = [1, 1], 1
+        for up in self.dec.ups:
+            u *= up.stride[0]
+            mult.append(u)
+        return tuple(mult)
+
+    @torch.no_grad()
+    def infer_bucketed(self, x, emo, sid, noise, t_y, *, x_lengths=None, length_scale=1.0,
+                       noise_start=None):
+        """infer (models.py:537-556) / EmoVITS.infer (infer.py:160-182) with
+        NO host synchronisation, over a static bucket of t_y frames - the
+        whole utterance can be captured into one hipGraph
+        (capture_infer_bucketed).  The durations, y_len and the path are
+        computed on the device (ops.expand_durations: the exp / ceil / sum /
+        .item() / infer_path / expansion of models.py:544-553); the reverse
+        flow and the decoder run masked at y_len (every conv output is zero
+        past it, i.e. the zero padding the reference's decoder sees at the
+        utterance end) and tiles past y_len + 64 are skipped
+        (ops.length_skip), so the work follows y_len, not t_y.
+
+        ``noise``: pre-scaled like infer_p2's (z = m + noise * s): [B, C,
+        t_y], or a flat buffer read from ``noise_start`` (int32 [B]) as
+        EmoVITS slices it.  ``x_lengths`` (int32 [B]): padded text, encoded
+        as TextEncoder.infer of each unpadded utterance (every layer masked,
+        engine.TextEncoderPlan pad_exact); None: the exact-length infer_p1
+        path (B = 1).  Returns (wav [B, 1, t_y * hop], y_len int32 [B]);
+        samples past y_len * hop are not meaningful (crop on the host)."""
+        engine._check_gpu(x, "SynthesizerTrn.infer_bucketed")
+        dt = x.dtype
+        if x_lengths is None:
+            m_p, s_p, logw, g = self.infer_p1(x, emo, sid)
+            xl = None
+        else:
+            g = self.emb_g(sid)
+            xl = x_lengths.to(device=x.device, dtype=torch.int32).contiguous()
+            h, m_p, s_p = self.enc_p.forward_masked_hip(x, xl, emo, g, exp_logs=True,
+                                                        pad_exact=True)
+            logw = engine.get_plan(self.dp, engine.DurationPlan).run(h, g, lengths=xl)
+            m_p, s_p, logw = m_p.to(dt), s_p.to(dt), logw.to(dt)
+        z, lens = engine.ops.expand_durations(
+            logw, m_p, s_p, noise, int(t_y), rate=float(length_scale), x_len=xl,
+            noise_start=noise_start, half_round=dt == torch.float16,
+            stage_mult=self._stage_mult())
+        gf = engine._f32(g)
+        with engine.ops.length_skip(64):
+            engine.get_plan(self.flow, engine.CouplingFlowPlan).run_(z, gf, lengths=lens[0])
+            o = engine.get_plan(self.dec, engine.GeneratorPlan).run(z, gf, lengths=lens[1:])
+        return o.to(m_p.dtype), lens[0]
+
+    @torch.no_grad()
+    def capture_infer_bucketed(self, t_x, t_y, *, noise_len=None, padded_text=False,
+                               length_scale=1.0, warmup=2):
+        """One hipGraph for a whole utterance (infer_bucketed) of t_x tokens
+        (padded_text: up to t_x, x_lengths given at replay) into a t_y-frame
+        bucket.  noise_len: replay reads a flat noise buffer of that many
+        elements at a per-call start offset (EmoVITS); else noise [1, C,
+        t_y].  Returns run(x, emo, sid, noise, noise_start=None,
+        x_length=None) -> (wav, y_len) views of static buffers."""
+        dev = next(self.parameters()).device
+        dt = next(self.parameters()).dtype
+        C = self.inter_channels
+        static = dict(x=torch.zeros(1, t_x, self.text_channels, device=dev, dtype=dt),
+                      emo=torch.zeros(1, 1024, device=dev, dtype=dt),
+                      sid=torch.zeros(1, device=dev, dtype=torch.long),
+                      start=torch.zeros(1, device=dev, dtype=torch.int32),
+                      xl=torch.full((1,), t_x, device=dev, dtype=torch.int32),
+                      noise=torch.zeros(noise_len if noise_len else C * t_y, device=dev))
+
+        def body():
+            noise = static["noise"] if noise_len else static["noise"].view(1, C, t_y)
+            return self.infer_bucketed(static["x"], static["emo"], static["sid"], noise, t_y,
+                                       x_lengths=static["xl"] if padded_text else None,
+                                       length_scale=length_scale,
+                                       noise_start=static["start"] if noise_len else None)
+
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                body()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = body()
+
+        def run(x, emo, sid, noise=None, noise_start=0, x_length=None):
+            if padded_text:
+                n = x.shape[1] if x_length is None else int(x_length)
+                static["x"].zero_()
+                static["x"][:, :x.shape[1]].copy_(x)
+                static["xl"].fill_(n)
+            else:
+                static["x"].copy_(x)
+            static["emo"].copy_(emo)
+            static["sid"].copy_(sid)
+            if noise is not None:
+                static["noise"].copy_(noise.reshape(-1))
+            static["start"].fill_(int(noise_start))
+            graph.replay()
+            return out
+
+        run.graph = graph
+        run.static = static
+        run.t_y = t_y
+        return run
 
     # ------------------------------------------------------------ hipGraphs
     @torch.no_grad()

@@ -271,12 +271,18 @@ def split_planes(w: torch.Tensor) -> torch.Tensor:
     return torch.stack([h, m, lo], dim=-3).to(torch.bfloat16)
 
 
-# Split-fp32 layers need >= this many GEMM rows: the sweep above measured it
-# ahead of the exact-f32 kernel on every 128- / 256-channel decoder conv
-# (+8..35 %), the upsamplers, conv_pre and the flow, but behind it on the
-# 32-channel stage (k=3 65 vs 75, k=11 80 vs 108 TF/s); the 32- / 64-channel
-# stages keep exact fp32 and the fused ResBlock2-pair kernel.
-F32S_MIN_ROWS = 128
+# Split-fp32 layers need >= this many GEMM rows: the r02 sweep measured the
+# per-fragment split (F32S) ahead of the exact-f32 kernel on every 128- /
+# 256-channel decoder conv (+8..35 %), the upsamplers, conv_pre and the flow,
+# but behind it on the 32- / 64-channel stages.  With pre-split weights
+# (F32P, tools/conv_bench.py on MI355X, r03) the 64-channel stage gains too
+# (k=11 c1 180 vs 122 TF/s exact, c2 138 vs 107, k=7 c1 154 vs 104; k=3 c2
+# 56 vs 60), the 32-channel one still does not (k=11 92 vs 108): 64 rows.
+F32S_MIN_ROWS = int(os.environ.get("VITS_F32S_MIN_ROWS", "0"))
+
+
+def _f32s_min_rows() -> int:
+    return F32S_MIN_ROWS or (64 if SPLIT_W else 128)
 
 
 def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
@@ -288,7 +294,7 @@ def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
     if layer.wdtype != WDT_F32 or wdtype == WDT_F32:
         return layer
     if wdtype == WDT_F32S:
-        if layer.m < F32S_MIN_ROWS:
+        if layer.m < _f32s_min_rows():
             return layer
         kc = 16
         w32 = layer.w[:layer.cin]
@@ -402,6 +408,29 @@ def make_out(y: torch.Tensor, *, act: int = ACT_NONE, res: Optional[torch.Tensor
 _LOWP_TORCH = {WDT_F16: torch.float16, WDT_BF16: torch.bfloat16}
 
 
+class _LenSkip(threading.local):
+    margin = 0
+
+
+LEN_SKIP = _LenSkip()
+
+
+@contextlib.contextmanager
+def length_skip(margin: int = 64):
+    """While active, descriptors built with ``lengths`` skip every tile that
+    starts ``margin`` or more positions past lengths[b] (no compute, no
+    write; vits_conv1d_desc.len_skip): the bucketed whole-utterance infer
+    then costs what the utterance needs, not what the bucket holds.
+    ``margin`` must exceed every consumer's input halo ((k - 1) * dil / 2 <=
+    25 in the decoder)."""
+    old = LEN_SKIP.margin
+    LEN_SKIP.margin = int(margin)
+    try:
+        yield
+    finally:
+        LEN_SKIP.margin = old
+
+
 def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Optional[ConvOut] = None,
               split: Optional[int] = None, tin: Optional[int] = None, n_out: Optional[int] = None,
               in_slope: float = 1.0, cond: Optional[torch.Tensor] = None, cond_offset: int = 0,
@@ -451,6 +480,7 @@ def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Option
     d.up_pad = layer.up_pad
     d.t_out = t_out
     d.lengths = _ptr(lengths)
+    d.len_skip = LEN_SKIP.margin if lengths is not None else 0
     d.out0 = out0
     if out1 is not None:
         d.out1 = out1
@@ -579,8 +609,10 @@ def _resblock_kc(ch: int, k: int, dil: int):
 def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch.Tensor, *,
                        cond: Optional[torch.Tensor] = None, cond_offset: int = 0,
                        in_slope: float = 0.1, accumulate: bool = False,
-                       post_div: float = 1.0) -> ResblockPairDesc:
-    """y = x + c2(gate(c1(lrelu(x)) + cond)) in one launch (modules.py:250-260)."""
+                       post_div: float = 1.0,
+                       lengths: Optional[torch.Tensor] = None) -> ResblockPairDesc:
+    """y = x + c2(gate(c1(lrelu(x)) + cond)) in one launch (modules.py:250-260);
+    ``lengths`` (int32 [B], device): the utterance ends there (zero past)."""
     assert x.dtype == torch.float32 and y.dtype == torch.float32 and x.stride(2) == 1
     C_, T = x.shape[1], x.shape[2]
     kc1, kc2 = _resblock_kc(C_, c1.k, c1.dil)
@@ -596,6 +628,8 @@ def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch
     d.b2 = _ptr(c2.bias)
     d.y, d.y_bstride, d.y_cstride = y.data_ptr(), y.stride(0), y.stride(1)
     d.accumulate, d.post_div = int(accumulate), float(post_div)
+    d.lengths = _ptr(lengths)
+    d.len_skip = LEN_SKIP.margin if lengths is not None else 0
     return d
 
 
@@ -706,6 +740,44 @@ def expand_prior(attn: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor, noise
                                 _stream_ptr(attn.device)),
           "vits_expand_prior")
     return out
+
+
+def expand_durations(logw: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor,
+                     noise: torch.Tensor, t_y: int, *, rate: float = 1.0,
+                     noise_scale: float = 1.0, x_len: Optional[torch.Tensor] = None,
+                     noise_start: Optional[torch.Tensor] = None, half_round: bool = False,
+                     stage_mult=(1,), out: Optional[torch.Tensor] = None,
+                     lens: Optional[torch.Tensor] = None):
+    """Durations -> (z [B, C, t_y], lens int32 [n_stage, B]) on the device,
+    without the host sync of models.py:547 / infer.py:171: w_ceil =
+    ceil(exp(logw) * rate), y_len = max(sum, 1), z = the one-hot expansion of
+    m_p + noise * s_p * noise_scale over the static bucket t_y (0 past
+    y_len), lens[i] = y_len * stage_mult[i].  ``noise`` is [B, C, t_y], or
+    with ``noise_start`` (int32 [B]) a flat buffer read as EmoVITS slices it
+    (element (c, t) at s + c * y_len + t, s = noise_start[b] mod (numel -
+    C * y_len): a raw random draw lands uniformly in the valid range)."""
+    require_device(logw, m_p, s_p, noise)
+    B, C_, t_x = m_p.shape
+    logw = logw.reshape(B, t_x).float().contiguous()
+    m_p = m_p.float().contiguous()
+    s_p = s_p.float().contiguous()
+    noise = noise.float().contiguous()
+    if out is None:
+        out = torch.empty(B, C_, t_y, device=m_p.device, dtype=torch.float32)
+    n_stage = len(stage_mult)
+    if lens is None:
+        lens = torch.empty(n_stage, B, device=m_p.device, dtype=torch.int32)
+    mult = (C.c_int32 * n_stage)(*[int(v) for v in stage_mult])
+    if noise_start is None:
+        assert tuple(noise.shape) == (B, C_, t_y), noise.shape
+    check(_lib.load().vits_expand_durations(
+        logw.data_ptr(), logw.stride(0), _ptr(x_len), t_x, float(rate), int(half_round),
+        m_p.data_ptr(), s_p.data_ptr(), m_p.stride(0), m_p.stride(1), noise.data_ptr(),
+        0 if noise_start is None else 1, _ptr(noise_start), noise.numel(), float(noise_scale),
+        out.data_ptr(),
+        B, C_, t_y, lens.data_ptr(), mult, n_stage, _stream_ptr(m_p.device)),
+        "vits_expand_durations")
+    return out, lens
 
 
 def conv_post_tanh(x: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Tensor] = None):
