@@ -25,6 +25,8 @@
 // Reference call sites: modules.py:136,148 (WN in/res_skip convs),
 // modules.py:252,257 (ResBlock2 convs1/convs2), models.py:307,310
 // (conv_pre, ups), modules.py:363,366 (coupling pre/post).
+#include <cstdlib>
+
 #include "conv1d_impl.h"
 
 namespace {
@@ -53,6 +55,27 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   return VITS_OK;
 }
 
+// 16-bit operand types read their weight fragments from global memory
+// (conv1d_impl.h GA) for fp32-activation (inference) groups with a >= 5-tap
+// member; tools/conv_bench.py BF=1 on MI355X (B=16, Ty=500): k = 7 / 11
+// +3..20 %, k = 3 -3..-15 % and the 2-tap upsampler -11 % against the
+// LDS-staged weights, and the fp16-I/O training convs (kc up to 64) lose
+// ~3 % of the train step.  VITS_GA16=0 / =2: never / always (A/B).
+bool ga16(const vits_conv1d_desc* d, int n) {
+  static const int mode = [] {
+    const char* e = getenv("VITS_GA16");
+    return e ? e[0] - '0' : 1;
+  }();
+  if (mode == 0) return false;
+  if (mode == 2) return true;
+  int kmax = 0;
+  for (int i = 0; i < n; ++i) {
+    if (d[i].io16) return false;
+    kmax = d[i].k > kmax ? d[i].k : kmax;
+  }
+  return kmax >= 5;
+}
+
 int conv1d_group(const vits_conv1d_desc* d, int n, int batch, hipStream_t s) {
   vits_conv::ConvGroup g;
   g.n = n;
@@ -64,9 +87,9 @@ int conv1d_group(const vits_conv1d_desc* d, int n, int batch, hipStream_t s) {
   }
   switch (d[0].wdtype) {
     case VITS_WDT_BF16:
-      return vits_conv1d_dispatch_bf16(g, s);
+      return ga16(d, n) ? vits_conv1d_dispatch_bf16g(g, s) : vits_conv1d_dispatch_bf16(g, s);
     case VITS_WDT_F16:
-      return vits_conv1d_dispatch_f16(g, s);
+      return ga16(d, n) ? vits_conv1d_dispatch_f16g(g, s) : vits_conv1d_dispatch_f16(g, s);
     case VITS_WDT_F32S:
       return vits_conv1d_dispatch_f32s(g, s);
     case VITS_WDT_F32P:

@@ -169,7 +169,8 @@ struct ConvGroup {
 // tensors of the operand type (the fp16-autocast training step keeps its
 // activations in fp16, as the reference's autocast convs return them),
 // half the bytes of the fp32-I/O kernel; accumulation stays fp32.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false,
+          bool GA = false>
 __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
   static_assert(!IO16 || WT != VITS_WDT_F32, "IO16 needs a 16-bit operand type");
   const int gi = (int)blockIdx.z / G.batch;
@@ -182,8 +183,11 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   // fragments loaded from the host-split bf16 planes in global memory, one
   // k-step ahead, into registers; LDS holds only the X window, double
   // buffered (one barrier per chunk); kc == 16, one chunk = one 16-channel slab
-  constexpr bool WG = WT == VITS_WDT_F32P;
-  constexpr bool SPL = WT == VITS_WDT_F32S || WG;
+  // GA (16-bit operand types): the same global-A structure on the packed
+  // 16-bit image [cin_pad/16][k][2][m_pad][8] (one plane)
+  static_assert(!GA || WT == VITS_WDT_BF16 || WT == VITS_WDT_F16, "GA: 16-bit types");
+  constexpr bool WG = WT == VITS_WDT_F32P || GA;
+  constexpr bool SPL = WT == VITS_WDT_F32S || WT == VITS_WDT_F32P;
   constexpr int WQ = SPL ? 8 : 4;  // float slots per (W row, 8 channels)
   // split fp32 on 128x128 tiles: the W chunk is staged pre-split as well
   // (three bf16 planes, one buffer; global -> registers under the MFMAs,
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   const bool act_in = slope != 1.0f;
   // (pre-split W, no W stage in LDS: the 16-bit activations' larger window
   // budget, i.e. 32-channel chunks on 128-column tiles)
-  constexpr bool XB = IO16 || WG;
+  constexpr bool XB = IO16 || WT == VITS_WDT_F32P;
   constexpr int MAXX = XTile<BN, BF, XB>::regs;
   // T4 staging (16-bit activations, V4 rows): a unit is 4 channels x 4 time
   // steps - four 8-byte row loads, transposed in registers into four 8-byte
@@ -525,64 +529,76 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   const int steps = k * half;  // MFMA k-steps per chunk
 
   if constexpr (WG) {
-    // ---- pre-split W from global (VITS_WDT_F32P) ----------------------------
+    // ---- W from global memory (VITS_WDT_F32P / GA) --------------------------
     // A chunk of kc = 16 G channels is G slabs; its k-steps run slab-major
     // (g, then tap j), so the flat step s = slab * k + j walks the weight
-    // image contiguously: the A fragments of step s (plane q, row r, half
-    // lhi) are the 16 bytes at
-    //   w + ((s * 2 + lhi) * 3 + q) * m_pad * 8 + r * 8   (bf16 elements),
+    // image contiguously: the A fragments of step s (plane q of NPL, row r,
+    // half lhi) are the 16 bytes at
+    //   w + ((s * 2 + lhi) * NPL + q) * m_pad * 8 + r * 8   (16-bit elements),
     // i.e. 32 consecutive rows = 512 contiguous bytes per load instruction.
+    // NPL = 3 (F32P: hi / mid / lo planes, six MFMAs per fragment pair) or 1
+    // (GA: the bf16 / fp16 image, one MFMA).
+    constexpr int NPL = SPL ? 3 : 1;
+    constexpr int NB = SPL ? TN : 1;  // (mid / lo B planes: split only)
+    typedef lpx8 av_t;
     const int G = kc >> 4;
     const int nst = G * k;  // k-steps per chunk
     const int total = nchunks * nst;
-    const __bf16* wbase = reinterpret_cast<const __bf16*>(p.w) +
-                          ((int64_t)(lhi * 3) * p.m_pad + m0 + wm + l32) * 8;
-    const int64_t wstep = (int64_t)48 * p.m_pad;
-    auto loadA = [&](int s, bf16x8_t (*a)[TM]) {
-      const __bf16* wp = wbase + (int64_t)(s < total ? s : total - 1) * wstep;
+    const lp_t* wbase = reinterpret_cast<const lp_t*>(p.w) +
+                        ((int64_t)(lhi * NPL) * p.m_pad + m0 + wm + l32) * 8;
+    const int64_t wstep = (int64_t)16 * NPL * p.m_pad;
+    auto loadA = [&](int s, av_t (*a)[TM]) {
+      const lp_t* wp = wbase + (int64_t)(s < total ? s : total - 1) * wstep;
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NPL; ++q)
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
-          a[q][mi] = *reinterpret_cast<const bf16x8_t*>(wp + ((int64_t)q * p.m_pad + mi * 32) * 8);
+          a[q][mi] = *reinterpret_cast<const av_t*>(wp + ((int64_t)q * p.m_pad + mi * 32) * 8);
     };
     // B fragments of tap j, slab g of the chunk: rows wn + ni*32 + l32 + j*dil
-    // of the [t][kcp] window planes, channels 16 g + 8 lhi .. + 8
-    const __bf16* const xlane0 = reinterpret_cast<const __bf16*>(xbuf1) +
-                                 (wn + l32 + xsh) * kcp + 8 * lhi;
-    const int xdelta = (int)(reinterpret_cast<const __bf16*>(xbuf2) -
-                             reinterpret_cast<const __bf16*>(xbuf1));
-    auto loadB = [&](int buf, int j, int g, bf16x8_t* bh, bf16x8_t* bm, bf16x8_t* bl) {
+    // of the [t][kcp] window plane(s), channels 16 g + 8 lhi .. + 8
+    const lp_t* const xlane0 = reinterpret_cast<const lp_t*>(xbuf1) +
+                               (wn + l32 + xsh) * kcp + 8 * lhi;
+    const int xdelta = (int)(reinterpret_cast<const lp_t*>(xbuf2) -
+                             reinterpret_cast<const lp_t*>(xbuf1));
+    auto loadB = [&](int buf, int j, int g, av_t* bh, av_t* bm, av_t* bl) {
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const lpx4* xp = reinterpret_cast<const lpx4*>(
             xlane0 + buf * xdelta + (ni * 32 + j * dil) * kcp + 16 * g);
-        const int P4 = xpl / 4;  // plane stride in 8-byte pieces
         bh[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
-        bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
-        bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+        if constexpr (SPL) {
+          const int P4 = xpl / 4;  // plane stride in 8-byte pieces
+          bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+          bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+        }
       }
     };
-    // the same six products in the same order as the F32S path (bitwise the
-    // same result for kc = 16): small terms first
-    auto mma = [&](bf16x8_t (*a)[TM], const bf16x8_t* bh, const bf16x8_t* bm,
-                   const bf16x8_t* bl) {
+    // split: the same six products in the same order as the F32S path
+    // (bitwise the same result): small terms first
+    auto mma = [&](av_t (*a)[TM], const av_t* bh, const av_t* bm, const av_t* bl) {
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
           f32x16 c = acc[mi][ni];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bl[ni], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][mi], bh[ni], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bm[ni], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bm[ni], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bh[ni], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bh[ni], c, 0, 0, 0);
+          if constexpr (SPL) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bl[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][mi], bh[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bm[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bm[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bh[ni], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bh[ni], c, 0, 0, 0);
+          } else if constexpr (WT == VITS_WDT_F16) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][mi], bh[ni], c, 0, 0, 0);
+          } else {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bh[ni], c, 0, 0, 0);
+          }
           acc[mi][ni] = c;
         }
     };
-    bf16x8_t a0[3][TM], a1[3][TM];
-    bf16x8_t bh0[TN], bm0[TN], bl0[TN], bh1[TN], bm1[TN], bl1[TN];
+    av_t a0[NPL][TM], a1[NPL][TM];
+    av_t bh0[TN], bm0[NB], bl0[NB], bh1[TN], bm1[NB], bl1[NB];
     loadA(0, a0);
     gload(0);
     lstore(xbuf1, 0);
@@ -625,7 +641,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, bh0, bm0, bl0);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < NPL; ++q)
 #pragma unroll
           for (int mi = 0; mi < TM; ++mi) a0[q][mi] = a1[q][mi];
       }
@@ -1044,27 +1060,27 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   }
 }
 
-template <int BM, int BN, int WM_, int WN_, int WT, bool V4, bool IO16>
+template <int BM, int BN, int WM_, int WN_, int WT, bool V4, bool IO16, bool GA = false>
 int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
   constexpr bool BF = WT != VITS_WDT_F32;
   size_t lds = 0;
   int gx = 0, gy = 0;
   for (int i = 0; i < g.n; ++i) {
     const vits_conv1d_desc& d = g.d[i];
-    constexpr bool WG = WT == VITS_WDT_F32P;
-    constexpr bool SPL = WT == VITS_WDT_F32S || WG;
+    constexpr bool WG = WT == VITS_WDT_F32P || GA;
+    constexpr bool SPL = WT == VITS_WDT_F32S || WT == VITS_WDT_F32P;
     const size_t wsz = WG ? 0 : (BF && !SPL) ? (size_t)d.kc * d.k * BM / 2 : (size_t)d.kc * d.k * BM;
     const size_t xsz = (size_t)d.kc * xrs[i];
     if (wsz > (size_t)(SPL ? (BM == 128 && BN == 128 ? VITS_W_TILE_WPS : VITS_W_TILE_SPL)
                            : BF ? VITS_W_TILE_BF : VITS_W_TILE) ||
-        xsz > (size_t)XTile<BN, BF, IO16 || WG>::floats)
+        xsz > (size_t)XTile<BN, BF, IO16 || WT == VITS_WDT_F32P>::floats)
       return VITS_E_UNSUP;
-    if (WG && d.kc != 16 && d.kc != 32) return VITS_E_UNSUP;
+    if (WT == VITS_WDT_F32P && d.kc != 16 && d.kc != 32) return VITS_E_UNSUP;
     // 32-bit window offsets
     if ((int64_t)d.kc * d.x_cstride + (int64_t)(d.tin + BN) * d.x_tstride >= (1LL << 31))
       return VITS_E_UNSUP;
     if (V4 && (IO16 || SPL)) {  // T4 staging: kc/4 channel quads x ceil(nb/4)*4 blocks
-      constexpr int nu = (XTile<BN, BF, IO16 || WG>::floats / 16 + 48 + 255) / 256;
+      constexpr int nu = (XTile<BN, BF, IO16 || WT == VITS_WDT_F32P>::floats / 16 + 48 + 255) / 256;
       if (d.kc % 16 || (size_t)d.kc * ((xrs[i] / 4 + 3) / 4) > (size_t)nu * 256)
         return VITS_E_UNSUP;
     }
@@ -1079,7 +1095,8 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     const size_t tail = SPL ? (size_t)(d.dil + 2) * (d.kc + 4) / 2 + 64
                             : 2 * (size_t)d.k * BM + 2 * xrs[i] + 64;
     // (WG: two X buffers, no W)
-    const size_t l = sizeof(float) * (wst + ((SPL && !WG) ? 1 : 2) * xslots + tail);
+    const size_t tail_wg = WG && !SPL ? (size_t)(d.dil + 2) * (d.kc + 4) / 2 + 64 : tail;
+    const size_t l = sizeof(float) * (wst + ((SPL && !WG) ? 1 : 2) * xslots + tail_wg);
     if (l > lds) lds = l;
     const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;
     if (x > gx) gx = x;
@@ -1092,15 +1109,15 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
   switch (d.epi) {
     case VITS_EPI_STORE:
       if (d.split < d.m)
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, WT, V4, IO16>), grid, block, lds, s, g);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, EPI_STORE2, WT, V4, IO16, GA>), grid, block, lds, s, g);
       else
-        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, WT, V4, IO16>), grid, block, lds, s, g);
+        hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_STORE, WT, V4, IO16, GA>), grid, block, lds, s, g);
       break;
     case VITS_EPI_GATE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, WT, V4, IO16>), grid, block, lds, s, g);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_GATE, WT, V4, IO16, GA>), grid, block, lds, s, g);
       break;
     case VITS_EPI_UPSAMPLE:
-      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, WT, V4, IO16>), grid, block, lds, s, g);
+      hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN, WM_, WN_, VITS_EPI_UPSAMPLE, WT, V4, IO16, GA>), grid, block, lds, s, g);
       break;
     default:
       return VITS_E_UNSUP;
@@ -1112,7 +1129,7 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
 // steps (the [B][C][T] activations with T % 4 == 0) and the wider window
 // still fits the stage; element-wise staging otherwise.  A group runs one
 // staging kind: mixed members are UNSUP (the caller launches them apart).
-template <int BM, int BN, int WM_, int WN_, int WT>
+template <int BM, int BN, int WM_, int WN_, int WT, bool GA = false>
 int launch_tile(const ConvGroup& g, hipStream_t s) {
   constexpr bool BF = WT != VITS_WDT_F32;
   size_t xrs4[VITS_CONV_GROUP], xrs1[VITS_CONV_GROUP];
@@ -1138,17 +1155,17 @@ int launch_tile(const ConvGroup& g, hipStream_t s) {
     return VITS_E_UNSUP;
   if constexpr (BF && WT != VITS_WDT_F32S && WT != VITS_WDT_F32P) {  // (split: fp32 I/O only)
     if (nio) {
-      if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, true>(g, s, xrs4);
+      if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, true, GA>(g, s, xrs4);
       if (nv4 != 0) return VITS_E_UNSUP;
-      return launch_tile_v<BM, BN, WM_, WN_, WT, false, true>(g, s, xrs1);
+      return launch_tile_v<BM, BN, WM_, WN_, WT, false, true, GA>(g, s, xrs1);
     }
   }
-  if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, false>(g, s, xrs4);
+  if (nv4 == g.n) return launch_tile_v<BM, BN, WM_, WN_, WT, true, false, GA>(g, s, xrs4);
   if (nv4 != 0) return VITS_E_UNSUP;
-  return launch_tile_v<BM, BN, WM_, WN_, WT, false, false>(g, s, xrs1);
+  return launch_tile_v<BM, BN, WM_, WN_, WT, false, false, GA>(g, s, xrs1);
 }
 
-template <int WT>
+template <int WT, bool GA = false>
 int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
   constexpr bool BF = WT != VITS_WDT_F32;
   const vits_conv1d_desc& d = g.d[0];
@@ -1167,11 +1184,11 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
       // a 128x128 grid that cannot fill the chip twice over (256 CUs) runs
       // as 64x128 tiles: same packing (its W/X budgets are a subset), twice
       // the workgroups
-      if (blocks < 512) return launch_tile<64, 128, 2, 2, WT>(g, s);
-      return launch_tile<128, 128, 2, 2, WT>(g, s);
+      if (blocks < 512) return launch_tile<64, 128, 2, 2, WT, GA>(g, s);
+      return launch_tile<128, 128, 2, 2, WT, GA>(g, s);
     }
     case VITS_TILE_64x128:
-      return launch_tile<64, 128, 2, 2, WT>(g, s);
+      return launch_tile<64, 128, 2, 2, WT, GA>(g, s);
     case VITS_TILE_64x256: {
       // same fallback for 64x256 grids (the flow / text-side convs at
       // T ~ 500) when the chunk's input window also fits the 128-column tile
@@ -1182,16 +1199,16 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
                                                           ? XTile<128, BF, true>::floats
                                                           : XTile<128, BF>::floats);
       }
-      if (blocks < 512 && fits128) return launch_tile<64, 128, 2, 2, WT>(g, s);
+      if (blocks < 512 && fits128) return launch_tile<64, 128, 2, 2, WT, GA>(g, s);
       if constexpr (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) {
         // split fp32: 2x2 waves (32x128 per wave) - each A-fragment split
         // feeds four B fragments instead of two (k=11 convs +1..3 %)
-        return launch_tile<64, 256, 2, 2, WT>(g, s);
+        return launch_tile<64, 256, 2, 2, WT, GA>(g, s);
       }
-      return launch_tile<64, 256, 1, 4, WT>(g, s);
+      return launch_tile<64, 256, 1, 4, WT, GA>(g, s);
     }
     case VITS_TILE_32x256:
-      return launch_tile<32, 256, 1, 4, WT>(g, s);
+      return launch_tile<32, 256, 1, 4, WT, GA>(g, s);
     default:
       return VITS_E_UNSUP;
   }
@@ -1205,3 +1222,5 @@ int vits_conv1d_dispatch_bf16(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_f16(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_f32s(const vits_conv::ConvGroup& g, hipStream_t s);
 int vits_conv1d_dispatch_f32p(const vits_conv::ConvGroup& g, hipStream_t s);
+int vits_conv1d_dispatch_bf16g(const vits_conv::ConvGroup& g, hipStream_t s);
+int vits_conv1d_dispatch_f16g(const vits_conv::ConvGroup& g, hipStream_t s);
