@@ -118,7 +118,8 @@ def pmc_traffic():
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes); None if absent."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))
+                   if not f.endswith(("_train_summary.json", "_longform_summary.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -153,9 +154,28 @@ def longform_leg(model, device, rank, steps=5, warmup=2, B=4, Tx=500, Ty=2500):
     noise = float(((out - ref) ** 2).sum())
     snr = 10.0 * math.log10(float((ref ** 2).sum()) / max(noise, 1e-30))
     samples = steps * B * Ty * HOP
+    # roofline: every conv launch of one eager bf16 step (HIP events per
+    # launch) against the dense bf16 MFMA peak; traffic: PMC HBM bytes per
+    # output frame of the replayed step (profiles/<tag>_longform_summary.json)
+    from vits_amd.ops import ConvTimer
+
+    with torch.no_grad(), ConvTimer() as timer:
+        m16.infer_p2(*inputs)
+    cs = timer.summary()
+    conv_tf = (cs["total_flops"] / 1e12) / (cs["total_ms"] / 1e3)
+    roof = {"bound": "mfma", "kernel": "every conv launch of the bf16 step",
+            "achieved": round(conv_tf, 1), "peak": FP16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(conv_tf / FP16_MFMA_PEAK_TFLOPS, 4),
+            "conv_ms_per_step": round(cs["total_ms"], 3)}
+    lf = _latest_summary("*_longform_summary.json")
+    if lf:
+        roof["traffic_bytes_per_frame"] = lf[0].get("hbm_bytes_per_frame")
+        roof["traffic"] = lf[0].get("hbm_bytes_per_step")
+        roof["traffic_source"] = lf[1]
+        roof["fused_minimum_bytes_per_frame"] = 160_000  # fp32 stage in/out once
     del m16
     torch.cuda.empty_cache()
-    return {"value": round(samples / el16, 1), "unit": "output samples/s",
+    return {"value": round(samples / el16, 1), "unit": "output samples/s", "roofline": roof,
             "ms_per_step": round(el16 / steps * 1e3, 3), "steps": steps, "warmup": warmup,
             "x_realtime_22k": round(samples / el16 / 22050.0, 1), "dtype": "bf16",
             "snr_db_vs_fp32": round(snr, 1),
@@ -358,6 +378,17 @@ def train_cpu_baseline(budget_s=10.0, B=4, max_steps=50):
 
 TRAIN_GFLOP_PER_UTT = 365.4  # FlopCounterMode, train_stft step, Tx=100 Ty=500
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 / bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def _latest_summary(pattern):
+    """(dict, relpath) of the newest committed profiles/<pattern>, or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
 def train_traffic():

@@ -138,7 +138,9 @@ typedef struct vits_conv1d_desc {
   float gmask_slope;
   /* io16 != 0 (16-bit wdtype only): x, out0/out1 y and res, and gmask are  */
   /* tensors of the 16-bit operand type (strides in elements); fp32 I/O    */
-  /* otherwise.  The fp16-autocast training convs keep fp16 activations.   */
+  /* otherwise.  The fp16-autocast training convs keep fp16 activations   */
+  /* (io16 = 1); io16 = 2 marks the 16-bit inference decoder, whose groups */
+  /* with a >= 5-tap member read weight fragments from global memory.    */
   int32_t io16;
   /* with lengths: > 0 = workgroups whose first output position is at or    */
   /* past lengths[b] + len_skip exit without computing or writing (the      */
@@ -217,6 +219,12 @@ int vits_expand_durations(const float* logw, int64_t logw_bstride, const int32_t
 
 int vits_conv_post_tanh(const float* x, int64_t x_bstride, int32_t x_cstride, const float* w,
                         float* y, int batch, int channels, int t_len, int ksize, void* stream);
+/* Same on a 16-bit last-stage activation (xdtype VITS_WDT_BF16 / _F16; the
+ * 16-bit model's decoder with 16-bit activations, as the reference's .half()
+ * model holds them); VITS_WDT_F32 = vits_conv_post_tanh. */
+int vits_conv_post_tanh_lowp(const void* x, int64_t x_bstride, int32_t x_cstride, const float* w,
+                             float* y, int batch, int channels, int t_len, int ksize, int xdtype,
+                             void* stream);
 
 /* ---------------------------------------------------------------------- */
 /* Monotonic alignment search (VITS DP + backtrack), bit-exact vs the     */

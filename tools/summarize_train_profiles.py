@@ -15,7 +15,8 @@ from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r03"
 batch = int(sys.argv[2]) if len(sys.argv) > 2 else 32
-src = os.path.join("gpurun_out", f"prof_{tag}_train")
+kind = sys.argv[3] if len(sys.argv) > 3 else "train"  # or "longform" (tools/run_longform_profiles.sh)
+src = os.path.join("gpurun_out", f"prof_{tag}_{kind}")
 
 
 def family(name):
@@ -75,8 +76,12 @@ summary = {"tag": tag, "batch": batch, "hbm_bytes_per_step": round(hbm),
                    "(gfx950 wide-read correction), KiB->B",
            "families": dict(sorted(fams.items(), key=lambda kv: -kv[1]["ms_per_step"]))}
 os.makedirs("profiles", exist_ok=True)
-with open(os.path.join("profiles", f"{tag}_train_summary.json"), "w") as fh:
+if kind == "longform":  # C5: B=4 x Ty=2500 frames per step
+    frames = batch * 2500
+    summary["frames_per_step"] = frames
+    summary["hbm_bytes_per_frame"] = round(hbm / frames)
+with open(os.path.join("profiles", f"{tag}_{kind}_summary.json"), "w") as fh:
     json.dump(summary, fh, indent=1)
 shutil.copy(os.path.join(src, "trace2", "run_kernel_stats.csv"),
-            os.path.join("profiles", f"{tag}_train_kernel_stats.csv"))
+            os.path.join("profiles", f"{tag}_{kind}_kernel_stats.csv"))
 print(json.dumps({k: v for k, v in summary.items() if k != "families"}, indent=1))

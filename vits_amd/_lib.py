@@ -233,6 +233,11 @@ _SIGS = {
         [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
          C.c_int, C.c_void_p],
     ),
+    "vits_conv_post_tanh_lowp": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+         C.c_int, C.c_int, C.c_void_p],
+    ),
     "vits_maximum_path": (
         C.c_int,
         [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,

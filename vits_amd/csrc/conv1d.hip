@@ -59,8 +59,10 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
 // (conv1d_impl.h GA) for fp32-activation (inference) groups with a >= 5-tap
 // member; tools/conv_bench.py BF=1 on MI355X (B=16, Ty=500): k = 7 / 11
 // +3..20 %, k = 3 -3..-15 % and the 2-tap upsampler -11 % against the
-// LDS-staged weights, and the fp16-I/O training convs (kc up to 64) lose
-// ~3 % of the train step.  VITS_GA16=0 / =2: never / always (A/B).
+// LDS-staged weights, and the fp16-I/O training convs (kc up to 64, io16 = 1)
+// lose ~3 % of the train step; the 16-bit-activation inference decoder
+// (io16 = 2) takes it for every group (C5, B=4 Ty=2500 bf16: conv time 12.9
+// -> 12.2 ms/step, its k=3 and 2-tap upsampler groups included).  VITS_GA16=0 / =2: never / always.
 bool ga16(const vits_conv1d_desc* d, int n) {
   static const int mode = [] {
     const char* e = getenv("VITS_GA16");
@@ -70,7 +72,8 @@ bool ga16(const vits_conv1d_desc* d, int n) {
   if (mode == 2) return true;
   int kmax = 0;
   for (int i = 0; i < n; ++i) {
-    if (d[i].io16) return false;
+    if (d[i].io16 == 1) return false;
+    if (d[i].io16 == 2) return true;
     kmax = d[i].k > kmax ? d[i].k : kmax;
   }
   return kmax >= 5;

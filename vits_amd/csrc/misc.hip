@@ -251,7 +251,10 @@ __global__ __launch_bounds__(256) void expand_durations_kernel(
 // ---------------------------------------------------------------------------
 constexpr int CP_T = 256;
 
-__global__ __launch_bounds__(256) void conv_post_tanh_kernel(const float* __restrict__ x,
+// XT: the activation type of the last stage (float; __bf16 / _Float16 when
+// the 16-bit model keeps its decoder activations 16-bit, engine.py ACT16)
+template <typename XT>
+__global__ __launch_bounds__(256) void conv_post_tanh_kernel(const XT* __restrict__ x,
                                                              int64_t x_bstride, int x_cstride,
                                                              const float* __restrict__ w,
                                                              float* __restrict__ y, int channels,
@@ -263,7 +266,7 @@ __global__ __launch_bounds__(256) void conv_post_tanh_kernel(const float* __rest
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * CP_T;
   const int pad = (ksize - 1) / 2;
-  const float* xb = x + (int64_t)b * x_bstride;
+  const XT* xb = x + (int64_t)b * x_bstride;
   for (int i = threadIdx.x; i < channels * ksize; i += 256) wsm[i] = w[i];
   // 8 channels x 2 window columns per thread in flight at once (a load-use
   // chain per element serialised ~2 x channels global latencies: 240 us for
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(256) void conv_post_tanh_kernel(const float* __rest
         const int t = threadIdx.x + 256 * h;
         const int tt = t0 - pad + t;
         const bool ok = c0 + cc < channels && t < W && tt >= 0 && tt < t_len;
-        v[cc][h] = ok ? xb[(int64_t)(c0 + cc) * x_cstride + tt] : 0.f;
+        v[cc][h] = ok ? (float)xb[(int64_t)(c0 + cc) * x_cstride + tt] : 0.f;
       }
 #pragma unroll
     for (int cc = 0; cc < CG; ++cc)
@@ -357,12 +360,31 @@ extern "C" int vits_expand_durations(const float* logw, int64_t logw_bstride,
 extern "C" int vits_conv_post_tanh(const float* x, int64_t x_bstride, int32_t x_cstride,
                                    const float* w, float* y, int batch, int channels, int t_len,
                                    int ksize, void* stream) {
+  return vits_conv_post_tanh_lowp(x, x_bstride, x_cstride, w, y, batch, channels, t_len, ksize,
+                                  VITS_WDT_F32, stream);
+}
+
+extern "C" int vits_conv_post_tanh_lowp(const void* x, int64_t x_bstride, int32_t x_cstride,
+                                        const float* w, float* y, int batch, int channels,
+                                        int t_len, int ksize, int xdtype, void* stream) {
   VITS_CHECK_ARG(x && w && y && batch > 0 && channels > 0 && t_len > 0 && ksize > 0);
+  VITS_CHECK_ARG(xdtype == VITS_WDT_F32 || xdtype == VITS_WDT_BF16 || xdtype == VITS_WDT_F16);
   VITS_CHECK_SHAPE((ksize & 1) == 1 && ksize <= 257 && x_cstride >= t_len);
   const size_t lds = sizeof(float) * ((size_t)channels * (CP_T + ksize - 1) + channels * ksize);
   VITS_CHECK_SHAPE(lds <= 64 * 1024);
   dim3 grid((t_len + CP_T - 1) / CP_T, batch);
-  hipLaunchKernelGGL(conv_post_tanh_kernel, grid, dim3(256), lds, as_stream(stream), x,
-                     x_bstride, x_cstride, w, y, channels, t_len, ksize);
+  hipStream_t s = as_stream(stream);
+  if (xdtype == VITS_WDT_BF16)
+    hipLaunchKernelGGL(conv_post_tanh_kernel<__bf16>, grid, dim3(256), lds, s,
+                       static_cast<const __bf16*>(x), x_bstride, x_cstride, w, y, channels, t_len,
+                       ksize);
+  else if (xdtype == VITS_WDT_F16)
+    hipLaunchKernelGGL(conv_post_tanh_kernel<_Float16>, grid, dim3(256), lds, s,
+                       static_cast<const _Float16*>(x), x_bstride, x_cstride, w, y, channels,
+                       t_len, ksize);
+  else
+    hipLaunchKernelGGL(conv_post_tanh_kernel<float>, grid, dim3(256), lds, s,
+                       static_cast<const float*>(x), x_bstride, x_cstride, w, y, channels, t_len,
+                       ksize);
   return vits_launch_status();
 }

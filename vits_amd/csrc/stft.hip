@@ -12,6 +12,8 @@
 // bins (upper bins 0), windowed into a per-frame workspace; a second kernel
 // overlap-adds the frames per sample (gather: no atomics, deterministic) and
 // folds the reflect padding back onto the signal.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -365,6 +367,174 @@ __device__ void stft_bwd_fold_block(const StftJobD& J, int jblk, int b) {
   J.gx[(int64_t)b * L + j] = g;
 }
 
+// ---------------------------------------------------------------------------
+// Forward, two-pass register FFT (n = N1 * N2, the four-step factorisation):
+//   pass 1, item (frame f, column t2):  Y[k1] = DFT_N1 over t1 of
+//           x[N2 t1 + t2] (loaded windowed + reflect-padded straight from
+//           global memory into registers), times W_n^{t2 k1} -> LDS
+//   pass 2, item (frame f, row k1):     X[k1 + N1 k2] = DFT_N2 over t2 of the
+//           LDS column, |X| (and re / im) of the one-sided bins -> global
+// Each point crosses LDS once (one write, one read, one barrier) instead of
+// once per radix-4 stage, and the DFTs run unrolled in registers with
+// compile-time twiddles; F frames per workgroup (F n = 4096 points).
+// LDS planes are [F][N2][N1 + 1] floats (re, im): odd row stride, no bank
+// conflicts on the column writes / row reads.
+// ---------------------------------------------------------------------------
+constexpr TwTable kTwC = make_tw();  // compile-time copy for the register DFTs
+
+constexpr int brev_c(int i, int logn) {
+  int r = 0;
+  for (int b = 0; b < logn; ++b) r |= ((i >> b) & 1) << (logn - 1 - b);
+  return r;
+}
+constexpr int ilog2_c(int n) { return n <= 1 ? 0 : 1 + ilog2_c(n >> 1); }
+
+// forward DFT (e^{-i}) of N <= 64 points held in registers, natural order in
+// and out: bit-reversed renaming, then radix-2 decimation in time; every
+// index and twiddle is a compile-time constant after unrolling
+template <int N>
+__device__ __forceinline__ void dft_reg(float (&xr)[N], float (&xi)[N]) {
+  constexpr int LN = ilog2_c(N);
+  float ar[N], ai[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    ar[brev_c(i, LN)] = xr[i];
+    ai[brev_c(i, LN)] = xi[i];
+  }
+#pragma unroll
+  for (int m = 2; m <= N; m <<= 1) {
+#pragma unroll
+    for (int k = 0; k < N; k += m) {
+#pragma unroll
+      for (int j = 0; j < m / 2; ++j) {
+        const int p = k + j, q = k + j + m / 2;
+        float vr, vi;
+        if (j == 0) {
+          vr = ar[q];
+          vi = ai[q];
+        } else if (4 * j == m) {  // W = -i
+          vr = ai[q];
+          vi = -ar[q];
+        } else {
+          const float c = kTwC.c[j * (FFT_MAX / m)];
+          const float sn = -kTwC.s[j * (FFT_MAX / m)];
+          vr = ar[q] * c - ai[q] * sn;
+          vi = ar[q] * sn + ai[q] * c;
+        }
+        const float ur = ar[p], ui = ai[p];
+        ar[p] = ur + vr;
+        ai[p] = ui + vi;
+        ar[q] = ur - vr;
+        ai[q] = ui - vi;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    xr[i] = ar[i];
+    xi[i] = ai[i];
+  }
+}
+
+template <int N1, int N2, int F>
+__device__ void stft_fwd2_block(const StftJobD& J, int fblk, int b, float* sm) {
+  constexpr int n = N1 * N2;
+  constexpr int YS = N1 + 1;
+  float* const twc = sm;  // W_n^m = cos - i sin (2 pi m / n), m < n
+  float* const tws = sm + n;
+  float* const yre = sm + 2 * n;
+  float* const yim = yre + F * N2 * YS;
+  for (int m = threadIdx.x; m < n; m += STFT_WG) {
+    const int h = m < n / 2 ? m : m - n / 2;
+    const float c = g_tw.c[h * (FFT_MAX / n)], sn = g_tw.s[h * (FFT_MAX / n)];
+    twc[m] = m < n / 2 ? c : -c;
+    tws[m] = m < n / 2 ? sn : -sn;
+  }
+  const int f0 = fblk * F;
+  const int woff = (n - J.win) / 2;
+  const float* xb = J.x + (int64_t)b * J.L;
+  __syncthreads();
+  for (int it = threadIdx.x; it < F * N2; it += STFT_WG) {
+    const int f = it / N2;
+    const int t2 = it - f * N2;
+    const int fr = f0 + f;
+    float xr[N1], xi[N1];
+#pragma unroll
+    for (int t1 = 0; t1 < N1; ++t1) {
+      const int t = N2 * t1 + t2;
+      const int wi = t - woff;
+      const bool ok = fr < J.frames && wi >= 0 && wi < J.win;
+      const int src = ok ? reflect_idx(fr * J.hop + t - J.pad, J.L) : 0;
+      xr[t1] = ok ? xb[src] * J.window[wi] : 0.f;
+      xi[t1] = 0.f;
+    }
+    dft_reg<N1>(xr, xi);
+    float* const ro = yre + (f * N2 + t2) * YS;
+    float* const io = yim + (f * N2 + t2) * YS;
+    ro[0] = xr[0];
+    io[0] = xi[0];
+#pragma unroll
+    for (int k1 = 1; k1 < N1; ++k1) {
+      const int m = t2 * k1;  // < n
+      const float c = twc[m], sn = -tws[m];
+      ro[k1] = xr[k1] * c - xi[k1] * sn;
+      io[k1] = xr[k1] * sn + xi[k1] * c;
+    }
+  }
+  __syncthreads();
+  const int nb = n / 2 + 1;
+  for (int it = threadIdx.x; it < F * N1; it += STFT_WG) {
+    int f, k1;
+    if (J.fmajor) {
+      f = it / N1;
+      k1 = it - f * N1;
+    } else {
+      k1 = it / F;
+      f = it - k1 * F;
+    }
+    const int fr = f0 + f;
+    float xr[N2], xi[N2];
+#pragma unroll
+    for (int t2 = 0; t2 < N2; ++t2) {
+      xr[t2] = yre[(f * N2 + t2) * YS + k1];
+      xi[t2] = yim[(f * N2 + t2) * YS + k1];
+    }
+    dft_reg<N2>(xr, xi);
+    if (fr >= J.frames) continue;
+#pragma unroll
+    for (int k2 = 0; k2 <= N2 / 2; ++k2) {
+      const int k = k1 + N1 * k2;
+      if (k < nb) {
+        const int64_t o = J.fmajor ? ((int64_t)b * J.frames + fr) * nb + k
+                                   : ((int64_t)b * nb + k) * J.frames + fr;
+        J.mag[o] = sqrtf(xr[k2] * xr[k2] + xi[k2] * xi[k2] + J.eps);
+        if (J.re) J.re[o] = xr[k2];
+        if (J.im) J.im[o] = xi[k2];
+      }
+    }
+  }
+}
+
+// (N1, N2, F) per size; 0 frames = size not covered (radix-4 Stockham path)
+__host__ __device__ constexpr int fwd2_frames(int n) {
+  // (2048 = 32 x 64 would need a 64-point register DFT: 256 VGPRs + scratch
+  // for the whole kernel, so it stays on the Stockham kernel)
+  return n == 128 ? 32 : n == 256 ? 16 : n == 512 ? 8 : n == 1024 ? 4 : 0;
+}
+size_t fwd2_lds(int n) {
+  const int n1 = n == 128 ? 16 : n == 256 ? 16 : n == 512 ? 16 : 32;
+  return sizeof(float) * (2 * n + 2 * fwd2_frames(n) * (n / n1) * (n1 + 1));
+}
+__device__ void stft_fwd2_any(const StftJobD& J, int fblk, int b, float* sm) {
+  switch (J.n) {
+    case 128: stft_fwd2_block<16, 8, 32>(J, fblk, b, sm); break;
+    case 256: stft_fwd2_block<16, 16, 16>(J, fblk, b, sm); break;
+    case 512: stft_fwd2_block<16, 32, 8>(J, fblk, b, sm); break;
+    case 1024: stft_fwd2_block<32, 32, 4>(J, fblk, b, sm); break;
+    default: break;
+  }
+}
+
 // ---- launch-level: one job (grid.y = utterance) or up to MAX_JOBS jobs in
 // one launch (grid.x runs over every job's blocks; a block finds its job in
 // the prefix table), so the ten transforms of an MR-STFT loss fill the chip
@@ -394,6 +564,19 @@ __global__ __launch_bounds__(256) void stft_fwd_multi_kernel(const StftJobs J) {
   const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
   const int b = local / J.per_b[j];
   stft_fwd_block(J.job[j], local - b * J.per_b[j], b, sfft);
+}
+
+__global__ __launch_bounds__(256) void stft_fwd2_kernel(const StftJobD J) {
+  extern __shared__ float sm2[];
+  stft_fwd2_any(J, blockIdx.x, blockIdx.y, sm2);
+}
+
+__global__ __launch_bounds__(256) void stft_fwd2_multi_kernel(const StftJobs J) {
+  extern __shared__ float sm2[];
+  const int j = find_job(J, blockIdx.x);
+  const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
+  const int b = local / J.per_b[j];
+  stft_fwd2_any(J.job[j], local - b * J.per_b[j], b, sm2);
 }
 
 __global__ __launch_bounds__(256) void stft_bwd_frames_kernel(const StftJobD J) {
@@ -453,6 +636,20 @@ int make_job(StftJobD& J, const float* x, int batch, int length, const float* wi
 size_t job_lds(const StftJobD& J) { return sizeof(float2) * (2 * J.fpb * J.n + J.n / 2); }
 int job_fblocks(const StftJobD& J) { return (J.frames + J.fpb - 1) / J.fpb; }
 
+// forward kind: the two-pass register FFT for n = 128 .. 2048 (VITS_STFT_FWD=1,
+// default), the radix-4 Stockham LDS FFT otherwise / VITS_STFT_FWD=0 (A/B)
+bool use_fwd2(int n) {
+  static const bool on = [] {
+    const char* e = getenv("VITS_STFT_FWD");
+    return !e || e[0] != '0';
+  }();
+  return on && fwd2_frames(n) > 0;
+}
+int fwd2_fblocks(const StftJobD& J) {
+  const int f = fwd2_frames(J.n);
+  return (J.frames + f - 1) / f;
+}
+
 }  // namespace
 
 extern "C" int64_t vits_stft_workspace(int batch, int length, int n_fft, int hop, int pad) {
@@ -472,6 +669,11 @@ extern "C" int vits_stft_mag_forward(const float* x, int batch, int length, cons
   J.mag = mag;
   J.re = re;
   J.im = im;
+  if (use_fwd2(n_fft)) {
+    hipLaunchKernelGGL(stft_fwd2_kernel, dim3(fwd2_fblocks(J), batch), dim3(256), fwd2_lds(n_fft),
+                       as_stream(stream), J);
+    return vits_launch_status();
+  }
   dim3 grid(job_fblocks(J), batch);
   hipLaunchKernelGGL(stft_fwd_kernel, grid, dim3(256), job_lds(J), as_stream(stream), J);
   return vits_launch_status();
@@ -503,26 +705,38 @@ extern "C" int vits_stft_mag_backward(const float* grad_mag, const float* mag, c
 
 extern "C" int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs, void* stream) {
   VITS_CHECK_ARG(jobs && njobs > 0 && njobs <= STFT_MAX_JOBS);
-  StftJobs M{};
-  M.njobs = njobs;
-  size_t lds = 0;
-  int blocks = 0;
+  // two launches at most: the sizes the two-pass kernel covers, the rest on
+  // the Stockham kernel (each launch walks its own job table)
+  StftJobs M[2] = {};
+  size_t lds[2] = {0, 0};
+  int blocks[2] = {0, 0};
   for (int i = 0; i < njobs; ++i) {
     const vits_stft_job& q = jobs[i];
     VITS_CHECK_ARG(q.x && q.mag);
-    int rc = make_job(M.job[i], q.x, q.batch, q.length, q.window, q.n_fft, q.hop, q.win, q.pad,
+    const int kind = use_fwd2(q.n_fft) ? 0 : 1;
+    StftJobs& S = M[kind];
+    const int j = S.njobs++;
+    int rc = make_job(S.job[j], q.x, q.batch, q.length, q.window, q.n_fft, q.hop, q.win, q.pad,
                       q.eps);
     if (rc) return rc;
-    M.job[i].mag = q.mag;
-    M.job[i].re = q.re;
-    M.job[i].im = q.im;
-    M.job[i].fmajor = q.layout;
-    M.per_b[i] = job_fblocks(M.job[i]);
-    blocks += M.per_b[i] * q.batch;
-    M.end[i] = blocks;
-    lds = job_lds(M.job[i]) > lds ? job_lds(M.job[i]) : lds;
+    S.job[j].mag = q.mag;
+    S.job[j].re = q.re;
+    S.job[j].im = q.im;
+    S.job[j].fmajor = q.layout;
+    S.per_b[j] = kind == 0 ? fwd2_fblocks(S.job[j]) : job_fblocks(S.job[j]);
+    blocks[kind] += S.per_b[j] * q.batch;
+    S.end[j] = blocks[kind];
+    const size_t l = kind == 0 ? fwd2_lds(q.n_fft) : job_lds(S.job[j]);
+    lds[kind] = l > lds[kind] ? l : lds[kind];
   }
-  hipLaunchKernelGGL(stft_fwd_multi_kernel, dim3(blocks), dim3(256), lds, as_stream(stream), M);
+  hipStream_t s = as_stream(stream);
+  if (M[0].njobs) {
+    hipLaunchKernelGGL(stft_fwd2_multi_kernel, dim3(blocks[0]), dim3(256), lds[0], s, M[0]);
+    int rc = vits_launch_status();
+    if (rc) return rc;
+  }
+  if (M[1].njobs)
+    hipLaunchKernelGGL(stft_fwd_multi_kernel, dim3(blocks[1]), dim3(256), lds[1], s, M[1]);
   return vits_launch_status();
 }
 

@@ -18,7 +18,8 @@ Reference semantics followed per plan (paths in emotional-vits/):
   PosteriorPlan      models.py:264-279 + modules.py:130-182
 
 Data layout in HBM: activations [B][C][T] fp32 exactly as the reference holds
-them; per-call intermediates come from the torch caching allocator.
+them (the Generator of a 16-bit model: [B][C][T] of that 16-bit type, ACT16);
+per-call intermediates come from the torch caching allocator.
 """
 from __future__ import annotations
 
@@ -125,6 +126,15 @@ _GROUP_BRANCHES = os.environ.get("VITS_GROUP_BRANCHES", "1") != "0"
 # fused ResBlock2 pairs on the 32/64-channel stages (VITS_FUSED_PAIRS=0: the
 # two-conv path, for A/B timing and the parity test of both)
 _FUSED_PAIRS = os.environ.get("VITS_FUSED_PAIRS", "1") != "0"
+# 16-bit models keep the decoder's activations 16-bit in HBM (as the
+# reference's .half() model holds them): every conv of the Generator reads and
+# writes its own 16-bit type (io16), halving the stage traffic.  C5 (B=4,
+# Ty=2500, bf16, MI355X): conv time 12.9 -> 12.2 ms/step, SNR vs the fp32
+# model 40.9 -> 39.0 dB (fp16: 56.2 dB).  The convs there are epilogue /
+# issue-bound rather than HBM-bound, so most of the gain is the global-memory
+# weight path these groups can take (conv1d.hip ga16, io16 = 2).
+# VITS_ACT16=0: fp32 activations (the 16-bit MFMA on fp32 I/O), for A/B.
+ACT16 = os.environ.get("VITS_ACT16", "1") != "0"
 
 
 class GeneratorPlan:
@@ -158,6 +168,14 @@ class GeneratorPlan:
         self.n_cond = conds.n
         self.post_w = _f32(gen.conv_post.weight)
         self.device = dev
+        lowp = {ops.WDT_BF16: torch.bfloat16, ops.WDT_F16: torch.float16}
+        self.act_dtype = lowp.get(self.conv_pre.wdtype, torch.float32) if ACT16 else torch.float32
+        if self.act_dtype != torch.float32:  # 16-bit X staging: wider K-chunks
+            layers = [self.conv_pre] + self.ups + [c for blocks in self.stages
+                                                   for pairs in blocks for pr in pairs
+                                                   for c in pr[:2]]
+            for layer in layers:
+                layer.kc = ops.io16_kc(layer)
 
     def conds(self, g: torch.Tensor) -> Optional[torch.Tensor]:
         if self.cond_w is None:
@@ -178,11 +196,13 @@ class GeneratorPlan:
             cond = self.conds(g)
         dev = x.device
         L = (lambda i: None) if lengths is None else (lambda i: lengths[i])
-        h = ops.conv1d(x, self.conv_pre, lengths=L(0))
+        # (16-bit activations: the conv rounds its input to the operand type
+        # anyway, so casting z first leaves conv_pre unchanged)
+        h = ops.conv1d(x.to(self.act_dtype), self.conv_pre, lengths=L(0))
         for i, (up, blocks) in enumerate(zip(self.ups, self.stages)):
             xu = ops.conv1d(h, up, in_slope=0.1, lengths=L(i + 1))
             C, T = xu.shape[1], xu.shape[2]
-            xs = torch.empty(B, C, T, device=dev, dtype=torch.float32)
+            xs = torch.empty(B, C, T, device=dev, dtype=xu.dtype)
             self._run_stage(blocks, xu, xs, cond, B, dev, L(i + 1))
             h = xs
         return ops.conv_post_tanh(h, self.post_w, out=out)
@@ -202,16 +222,17 @@ class GeneratorPlan:
         if any(len(pairs) != npairs for pairs in blocks):
             raise NotImplementedError("ResBlock2 branches with different dilation counts")
         C, T = xu.shape[1], xu.shape[2]
-        fused = [[_FUSED_PAIRS and ops.resblock_pair_supported(pr[0], pr[1], T) for pr in pairs]
-                 for pairs in blocks]
+        io16 = 2 if xu.dtype != torch.float32 else 0  # (2: inference decoder, conv1d.hip ga16)
+        fused = [[_FUSED_PAIRS and not io16 and ops.resblock_pair_supported(pr[0], pr[1], T)
+                  for pr in pairs] for pairs in blocks]
         tmp = [[torch.empty_like(xs), torch.empty_like(xs)] for _ in range(nk)]
         gbuf = [None if all(fused[j]) else
-                torch.empty(B, C // 2, T, device=dev, dtype=torch.float32) for j in range(nk)]
+                torch.empty(B, C // 2, T, device=dev, dtype=xu.dtype) for j in range(nk)]
         cur = [xu] * nk
 
         def c1_desc(j, p):
             return make_desc(blocks[j][p][0], cur[j], make_out(gbuf[j]), in_slope=0.1, cond=cond,
-                             cond_offset=blocks[j][p][2], lengths=lengths)
+                             cond_offset=blocks[j][p][2], lengths=lengths, io16=io16)
 
         def grouped(ds):
             return [tuple(ds)] if _GROUP_BRANCHES else list(ds)
@@ -230,7 +251,8 @@ class GeneratorPlan:
                 if cj:
                     descs = grouped(c1_desc(j, p) for j in cj)
                     descs += grouped(make_desc(blocks[j][p][1], gbuf[j],
-                                               make_out(dst[j], res=cur[j]), lengths=lengths)
+                                               make_out(dst[j], res=cur[j]), lengths=lengths,
+                                               io16=io16)
                                      for j in cj)
                     ops.conv1d_launch_seq(descs, B, dev)
                 cur = dst
@@ -248,7 +270,7 @@ class GeneratorPlan:
                 else:
                     ops.conv1d_launch_seq([make_desc(blocks[j][p][1], gbuf[j],
                                                      make_out(xs, res=cur[j], **kw),
-                                                     lengths=lengths)], B, dev)
+                                                     lengths=lengths, io16=io16)], B, dev)
 
 
 # ---------------------------------------------------------------------------

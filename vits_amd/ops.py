@@ -329,6 +329,28 @@ def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
                       wdtype=wdtype)
 
 
+# K-chunk of 16-bit inference layers whose activations are 16-bit too
+# (engine.ACT16): the X window of a chunk stages at 2 bytes per element, so a
+# chunk can hold 32-64 channels instead of 16 (fewer barriers per tile).
+# VITS_LOWP_KCK caps kc * k (16: keep kc = 16, for A/B).
+LOWP_KCK = int(os.environ.get("VITS_LOWP_KCK", "512"))
+
+
+def io16_kc(layer: PackedConv) -> int:
+    """Largest kc in (64, 48, 32, 16) dividing cin_pad that fits the kernel's
+    W stage (kc*k*BM/2 <= 6144 slots, for the LDS-weight groups) and the
+    16-bit X budget (conv1d_impl.h XTile<BN, BF, true>: 6144 / 10240
+    elements for BN 128 / 256)."""
+    bm, bn = TILE_ROWS[layer.tile], TILE_COLS[layer.tile]
+    xrs = bn + (layer.k - 1) * layer.dil + 8
+    xbudget = 6144 if bn <= 128 else 10240
+    for kc in (64, 48, 32):
+        if (kc * layer.k <= LOWP_KCK and layer.cin_pad % kc == 0
+                and kc * layer.k * bm // 2 <= 6144 and kc * xrs <= xbudget):
+            return kc
+    return 16
+
+
 def to_bf16(layer: PackedConv) -> PackedConv:
     return to_lowp(layer, WDT_BF16)
 
@@ -437,7 +459,8 @@ def make_desc(layer: PackedConv, x: torch.Tensor, out0: ConvOut, *, out1: Option
               lengths: Optional[torch.Tensor] = None, t_out: int = 0,
               x_channel_offset: int = 0, io16: bool = False) -> ConvDesc:
     """io16: x / outputs / residuals / gmask are tensors of the layer's
-    16-bit operand type (the fp16 training convs); fp32 otherwise."""
+    16-bit operand type - 1 (True) the fp16 training convs, 2 the 16-bit
+    inference decoder (csrc/conv1d.hip ga16); fp32 otherwise."""
     if io16:
         assert layer.wdtype != WDT_F32 and x.dtype == _LOWP_TORCH[layer.wdtype]
     else:
@@ -683,20 +706,24 @@ def conv1d(x: torch.Tensor, layer: PackedConv, *, in_slope: float = 1.0, act: in
            res_scale: float = 1.0, lengths: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, accumulate: bool = False,
            post_div: float = 1.0, t_out: Optional[int] = None) -> torch.Tensor:
-    """Run one packed conv on [B, cin, T] fp32 (device) and return [B, out_channels, T_out]."""
+    """Run one packed conv on [B, cin, T] (device) and return [B, out_channels,
+    T_out].  x fp32, or of the layer's 16-bit type (io16: output, residual
+    and accumulator of that type too)."""
     require_device(x, cond, residual, lengths)
     B, _, T = x.shape
+    io16 = x.dtype != torch.float32
     if layer.epi == EPI_UPSAMPLE:
         T_out = T * layer.up_u if t_out is None else t_out
     else:
         T_out = T
     if out is None:
-        out = torch.empty(B, layer.out_channels, T_out, device=x.device, dtype=torch.float32)
+        out = torch.empty(B, layer.out_channels, T_out, device=x.device, dtype=x.dtype)
     o0 = make_out(out, act=act, res=residual, res_scale=res_scale, accumulate=accumulate,
                   post_div=post_div)
     if lengths is not None:
         lengths = lengths.to(device=x.device, dtype=torch.int32).contiguous()
-    d = make_desc(layer, x, o0, in_slope=in_slope, cond=cond, lengths=lengths, t_out=T_out)
+    d = make_desc(layer, x, o0, in_slope=in_slope, cond=cond, lengths=lengths, t_out=T_out,
+                  io16=2 if io16 else 0)
     conv1d_launch(d, B, x.device)
     return out
 
@@ -787,10 +814,11 @@ def conv_post_tanh(x: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Te
     w = weight.reshape(Cc, k).contiguous().float()
     if out is None:
         out = torch.empty(B, 1, T, device=x.device, dtype=torch.float32)
+    xdt = {torch.float32: WDT_F32, torch.bfloat16: WDT_BF16, torch.float16: WDT_F16}[x.dtype]
     lib = _lib.load()
-    check(lib.vits_conv_post_tanh(x.data_ptr(), x.stride(0), x.stride(1), w.data_ptr(),
-                                  out.data_ptr(), B, Cc, T, k, _stream_ptr(x.device)),
-          "vits_conv_post_tanh")
+    check(lib.vits_conv_post_tanh_lowp(x.data_ptr(), x.stride(0), x.stride(1), w.data_ptr(),
+                                       out.data_ptr(), B, Cc, T, k, xdt, _stream_ptr(x.device)),
+          "vits_conv_post_tanh_lowp")
     return out
 
 
