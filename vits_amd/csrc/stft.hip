@@ -436,38 +436,58 @@ __device__ __forceinline__ void dft_reg(float (&xr)[N], float (&xi)[N]) {
   }
 }
 
-template <int N1, int N2, int F>
+// SP2: pass 2 as two half-size DFTs per row (radix-2 decimation in
+// frequency: even bins = DFT_{N2/2}(y[t] + y[t + N2/2]), odd bins =
+// DFT_{N2/2}((y[t] - y[t + N2/2]) W_N2^t)), one per thread - keeps n = 2048
+// (N2 = 64) at the register footprint of a 32-point DFT
+template <int N1, int N2, int F, bool SP2 = false>
 __device__ void stft_fwd2_block(const StftJobD& J, int fblk, int b, float* sm) {
   constexpr int n = N1 * N2;
   constexpr int YS = N1 + 1;
+  static_assert(F * N2 <= STFT_WG, "one pass-1 item per thread (the staging aliases Y)");
   float* const twc = sm;  // W_n^m = cos - i sin (2 pi m / n), m < n
   float* const tws = sm + n;
   float* const yre = sm + 2 * n;
   float* const yim = yre + F * N2 * YS;
+  // the workgroup's signal segment (its F frames overlap by n - hop) and the
+  // zero-extended window, staged once with coalesced loads (reflect padding
+  // applied here); aliased by Y after every thread holds its column
+  float* const xs = sm + 2 * n;
+  const int f0 = fblk * F;
+  const int seg0 = f0 * J.hop - J.pad;
+  const int seglen = (F - 1) * J.hop + n;
+  float* const ws = xs + seglen;
+  const int woff = (n - J.win) / 2;
+  const float* xb = J.x + (int64_t)b * J.L;
   for (int m = threadIdx.x; m < n; m += STFT_WG) {
     const int h = m < n / 2 ? m : m - n / 2;
     const float c = g_tw.c[h * (FFT_MAX / n)], sn = g_tw.s[h * (FFT_MAX / n)];
     twc[m] = m < n / 2 ? c : -c;
     tws[m] = m < n / 2 ? sn : -sn;
+    const int wi = m - woff;
+    ws[m] = (wi >= 0 && wi < J.win) ? J.window[wi] : 0.f;
   }
-  const int f0 = fblk * F;
-  const int woff = (n - J.win) / 2;
-  const float* xb = J.x + (int64_t)b * J.L;
+  for (int i = threadIdx.x; i < seglen; i += STFT_WG) {
+    const int t = seg0 + i;
+    xs[i] = (t >= -J.pad && t < J.L + J.pad) ? xb[reflect_idx(t, J.L)] : 0.f;
+  }
   __syncthreads();
-  for (int it = threadIdx.x; it < F * N2; it += STFT_WG) {
-    const int f = it / N2;
-    const int t2 = it - f * N2;
-    const int fr = f0 + f;
-    float xr[N1], xi[N1];
+  const int it = threadIdx.x;
+  const bool act1 = it < F * N2;
+  const int f = it / N2;
+  const int t2 = it - f * N2;
+  float xr[N1], xi[N1];
+  if (act1) {
+    const bool live = f0 + f < J.frames;
 #pragma unroll
     for (int t1 = 0; t1 < N1; ++t1) {
       const int t = N2 * t1 + t2;
-      const int wi = t - woff;
-      const bool ok = fr < J.frames && wi >= 0 && wi < J.win;
-      const int src = ok ? reflect_idx(fr * J.hop + t - J.pad, J.L) : 0;
-      xr[t1] = ok ? xb[src] * J.window[wi] : 0.f;
+      xr[t1] = live ? xs[f * J.hop + t] * ws[t] : 0.f;
       xi[t1] = 0.f;
     }
+  }
+  __syncthreads();  // Y overwrites the staged segment
+  if (act1) {
     dft_reg<N1>(xr, xi);
     float* const ro = yre + (f * N2 + t2) * YS;
     float* const io = yim + (f * N2 + t2) * YS;
@@ -483,6 +503,56 @@ __device__ void stft_fwd2_block(const StftJobD& J, int fblk, int b, float* sm) {
   }
   __syncthreads();
   const int nb = n / 2 + 1;
+  if constexpr (SP2) {
+    constexpr int H = N2 / 2;
+    for (int it = threadIdx.x; it < 2 * F * N1; it += STFT_WG) {
+      const int par = it & 1;  // neighbouring lanes: even / odd bins of one row
+      const int r = it >> 1;
+      int f, k1;
+      if (J.fmajor) {
+        f = r / N1;
+        k1 = r - f * N1;
+      } else {
+        k1 = r / F;
+        f = r - k1 * F;
+      }
+      const int fr = f0 + f;
+      float xr[H], xi[H];
+#pragma unroll
+      for (int t = 0; t < H; ++t) {
+        const float ar = yre[(f * N2 + t) * YS + k1], ai = yim[(f * N2 + t) * YS + k1];
+        const float br = yre[(f * N2 + t + H) * YS + k1], bi = yim[(f * N2 + t + H) * YS + k1];
+        if (par == 0) {
+          xr[t] = ar + br;
+          xi[t] = ai + bi;
+        } else {
+          const float dr = ar - br, di = ai - bi;
+          if (t == 0) {
+            xr[t] = dr;
+            xi[t] = di;
+          } else {
+            const float c = kTwC.c[t * (FFT_MAX / N2)], sn = -kTwC.s[t * (FFT_MAX / N2)];
+            xr[t] = dr * c - di * sn;
+            xi[t] = dr * sn + di * c;
+          }
+        }
+      }
+      dft_reg<H>(xr, xi);
+      if (fr >= J.frames) continue;
+#pragma unroll
+      for (int q = 0; q <= H / 2; ++q) {
+        const int k = k1 + N1 * (2 * q + par);
+        if (k < nb) {
+          const int64_t o = J.fmajor ? ((int64_t)b * J.frames + fr) * nb + k
+                                     : ((int64_t)b * nb + k) * J.frames + fr;
+          J.mag[o] = sqrtf(xr[q] * xr[q] + xi[q] * xi[q] + J.eps);
+          if (J.re) J.re[o] = xr[q];
+          if (J.im) J.im[o] = xi[q];
+        }
+      }
+    }
+    return;
+  }
   for (int it = threadIdx.x; it < F * N1; it += STFT_WG) {
     int f, k1;
     if (J.fmajor) {
@@ -517,13 +587,14 @@ __device__ void stft_fwd2_block(const StftJobD& J, int fblk, int b, float* sm) {
 
 // (N1, N2, F) per size; 0 frames = size not covered (radix-4 Stockham path)
 __host__ __device__ constexpr int fwd2_frames(int n) {
-  // (2048 = 32 x 64 would need a 64-point register DFT: 256 VGPRs + scratch
-  // for the whole kernel, so it stays on the Stockham kernel)
-  return n == 128 ? 32 : n == 256 ? 16 : n == 512 ? 8 : n == 1024 ? 4 : 0;
+  return n == 128 ? 32 : n == 256 ? 16 : n == 512 ? 8 : n == 1024 ? 4 : n == 2048 ? 2 : 0;
 }
-size_t fwd2_lds(int n) {
+size_t fwd2_lds(int n, int hop) {
   const int n1 = n == 128 ? 16 : n == 256 ? 16 : n == 512 ? 16 : 32;
-  return sizeof(float) * (2 * n + 2 * fwd2_frames(n) * (n / n1) * (n1 + 1));
+  const int F = fwd2_frames(n);
+  const int y = 2 * F * (n / n1) * (n1 + 1);  // Y planes
+  const int st = (F - 1) * hop + 2 * n;         // staged segment + window (aliased by Y)
+  return sizeof(float) * (2 * n + (y > st ? y : st));
 }
 __device__ void stft_fwd2_any(const StftJobD& J, int fblk, int b, float* sm) {
   switch (J.n) {
@@ -531,6 +602,7 @@ __device__ void stft_fwd2_any(const StftJobD& J, int fblk, int b, float* sm) {
     case 256: stft_fwd2_block<16, 16, 16>(J, fblk, b, sm); break;
     case 512: stft_fwd2_block<16, 32, 8>(J, fblk, b, sm); break;
     case 1024: stft_fwd2_block<32, 32, 4>(J, fblk, b, sm); break;
+    case 2048: stft_fwd2_block<32, 64, 2, true>(J, fblk, b, sm); break;
     default: break;
   }
 }
@@ -572,6 +644,16 @@ __global__ __launch_bounds__(256) void stft_fwd2_kernel(const StftJobD J) {
 }
 
 __global__ __launch_bounds__(256) void stft_fwd2_multi_kernel(const StftJobs J) {
+  extern __shared__ float sm2[];
+  const int j = find_job(J, blockIdx.x);
+  const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
+  const int b = local / J.per_b[j];
+  stft_fwd2_any(J.job[j], local - b * J.per_b[j], b, sm2);
+}
+
+// same, register budget capped at 4 waves per SIMD (A/B: VITS_STFT_OCC=4)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void stft_fwd2_multi_kernel_o4(const StftJobs J) {
   extern __shared__ float sm2[];
   const int j = find_job(J, blockIdx.x);
   const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
@@ -638,12 +720,12 @@ int job_fblocks(const StftJobD& J) { return (J.frames + J.fpb - 1) / J.fpb; }
 
 // forward kind: the two-pass register FFT for n = 128 .. 2048 (VITS_STFT_FWD=1,
 // default), the radix-4 Stockham LDS FFT otherwise / VITS_STFT_FWD=0 (A/B)
-bool use_fwd2(int n) {
+bool use_fwd2(int n, int hop) {
   static const bool on = [] {
     const char* e = getenv("VITS_STFT_FWD");
     return !e || e[0] != '0';
   }();
-  return on && fwd2_frames(n) > 0;
+  return on && fwd2_frames(n) > 0 && hop <= n && fwd2_lds(n, hop) <= 64 * 1024;
 }
 int fwd2_fblocks(const StftJobD& J) {
   const int f = fwd2_frames(J.n);
@@ -669,8 +751,8 @@ extern "C" int vits_stft_mag_forward(const float* x, int batch, int length, cons
   J.mag = mag;
   J.re = re;
   J.im = im;
-  if (use_fwd2(n_fft)) {
-    hipLaunchKernelGGL(stft_fwd2_kernel, dim3(fwd2_fblocks(J), batch), dim3(256), fwd2_lds(n_fft),
+  if (use_fwd2(n_fft, hop)) {
+    hipLaunchKernelGGL(stft_fwd2_kernel, dim3(fwd2_fblocks(J), batch), dim3(256), fwd2_lds(n_fft, hop),
                        as_stream(stream), J);
     return vits_launch_status();
   }
@@ -713,7 +795,7 @@ extern "C" int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs,
   for (int i = 0; i < njobs; ++i) {
     const vits_stft_job& q = jobs[i];
     VITS_CHECK_ARG(q.x && q.mag);
-    const int kind = use_fwd2(q.n_fft) ? 0 : 1;
+    const int kind = use_fwd2(q.n_fft, q.hop) ? 0 : 1;
     StftJobs& S = M[kind];
     const int j = S.njobs++;
     int rc = make_job(S.job[j], q.x, q.batch, q.length, q.window, q.n_fft, q.hop, q.win, q.pad,
@@ -726,12 +808,19 @@ extern "C" int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs,
     S.per_b[j] = kind == 0 ? fwd2_fblocks(S.job[j]) : job_fblocks(S.job[j]);
     blocks[kind] += S.per_b[j] * q.batch;
     S.end[j] = blocks[kind];
-    const size_t l = kind == 0 ? fwd2_lds(q.n_fft) : job_lds(S.job[j]);
+    const size_t l = kind == 0 ? fwd2_lds(q.n_fft, q.hop) : job_lds(S.job[j]);
     lds[kind] = l > lds[kind] ? l : lds[kind];
   }
   hipStream_t s = as_stream(stream);
   if (M[0].njobs) {
-    hipLaunchKernelGGL(stft_fwd2_multi_kernel, dim3(blocks[0]), dim3(256), lds[0], s, M[0]);
+    static const bool o4 = [] {
+      const char* e = getenv("VITS_STFT_OCC");
+      return e && e[0] == '4';
+    }();
+    if (o4)
+      hipLaunchKernelGGL(stft_fwd2_multi_kernel_o4, dim3(blocks[0]), dim3(256), lds[0], s, M[0]);
+    else
+      hipLaunchKernelGGL(stft_fwd2_multi_kernel, dim3(blocks[0]), dim3(256), lds[0], s, M[0]);
     int rc = vits_launch_status();
     if (rc) return rc;
   }
