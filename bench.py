@@ -512,10 +512,12 @@ def fp32_arith() -> str:
 
     if engine.FP32_MODE == "exact":
         return "exact: v_mfma_f32_32x32x2_f32 (bitwise an fp32 fma chain)"
-    return ("split: convs with >= 128 GEMM rows split each fp32 operand exactly into three "
-            "bf16 terms, six bf16 MFMAs per product, fp32 accumulation (error vs fp64 at or "
-            "below the exact-f32 kernel's, tests/test_kernels_gpu.py); the 32/64-channel "
-            "stages exact f32")
+    from vits_amd import ops
+
+    return (f"split: convs with >= {ops._f32s_min_rows()} GEMM rows split each fp32 operand "
+            "exactly into three bf16 terms (weights pre-split into planes), six bf16 MFMAs per "
+            "product, fp32 accumulation (error vs fp64 at or below the exact-f32 kernel's, "
+            "tests/test_kernels_gpu.py); the 32-channel stage exact f32")
 
 
 def _launch_ranks(args) -> int:

@@ -25,8 +25,27 @@ Fixtures (npz, float32 unless noted):
   mrstft.npz          stft_loss.MultiResolutionSTFTLoss on x,y [2, 9216]:
                       sc, mag, magnitude maps of resolutions 0 and 4
                       (utterance 0), per-resolution sums, d(sc+mag)/dy_hat.
+  mwsd.npz            mrd.MultiWaveSTFTDiscriminator (train_stft.py's D) on
+                      y, y_hat [2, 1, 3072] and their MR-STFT magnitudes:
+                      every score, dL_gen/dy_hat and d/dmag heads, parameter
+                      gradient statistics (norm, sum, abs-sum, max) plus the
+                      full gradients of the small tensors, the spectral-norm
+                      u vectors after one train-mode forward;
+                      mwsd_state_dict_shapes.json its keys -> shapes.
+  train_step.npz      ONE train_stft.py step (lines 162-236) on a tiny config
+                      (p_dropout 0, B=2, Tx 10, Ty 40, 16-frame segments):
+                      every RNG draw recorded (rand_slice, align noise,
+                      randn_like), losses, G / D gradient norms, per-parameter
+                      gradient statistics and post-step parameter statistics
+                      (RAdam for D, AdamW for G as the reference builds them);
+                      train_step_config.json the config.
+  base_c1.npz         the C1 headline utterance (configs/base.json, Tx=100,
+                      Ty=500, models.py:568-575): infer_p1 / infer_p2 outputs,
+                      waveform head / middle windows, per-block rms of the
+                      decoder, z statistics; plus SynthesizerTrn.infer at
+                      Tx=12 with its noise draw recorded.
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [mpd|mwsd|train_step|c1 ...]
 """
 from __future__ import annotations
 
