@@ -72,7 +72,7 @@ summary = {"tag": tag, "batch": batch, "hbm_bytes_per_step": round(hbm),
            "hbm_write_bytes_per_step": round(sum(w.values())),
            "dispatches_per_step": round(sum(v["dispatches_per_step"] for v in fams.values()), 1),
            "kernel_ms_per_step": round(tot_ms, 3),
-           "note": "(R=2 replays - R=1 replay) of the captured train_stft step; FETCH_SIZE x2 "
+           "note": f"(R=2 replays - R=1 replay) of the captured {'C5 long-form infer_p2' if kind == 'longform' else 'train_stft'} step; FETCH_SIZE x2 "
                    "(gfx950 wide-read correction), KiB->B",
            "families": dict(sorted(fams.items(), key=lambda kv: -kv[1]["ms_per_step"]))}
 os.makedirs("profiles", exist_ok=True)
