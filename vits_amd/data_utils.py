@@ -6,13 +6,151 @@
   per-epoch shuffles, rank r takes ids[r::world].
 * ``TextAudioSpeakerCollate`` — zero-pad collate sorted by spec length
   (data_utils.py:105-163).
+* ``TextAudioSpeakerLoader`` — the reference's filelist dataset
+  (data_utils.py:15-102): ``vec|wav|emo|sid`` lines, length filter, the
+  seed-1234 shuffle, items ``(vec[N,c], spec[F,T], wav[1,L], emo[1024],
+  sid[1])`` with the linear spectrogram read from the ``<wav>.spec.pt``
+  cache (data_utils.py:73-81).
+* ``build_spec_cache`` — the MI355X side of that cache: the reference
+  computes a missing spectrogram with ``torch.stft`` inside one of its 8
+  forked CPU loader workers and saves it; here the whole filelist's missing
+  caches are computed up front in the main process on the GPU (one HIP STFT
+  launch per run of equal-length utterances) and written in the reference's
+  ``.spec.pt`` format, so the workers only ever load.  A loader worker never
+  initialises HIP (a forked child of a HIP process cannot use the device).
 * ``SyntheticTextAudioSpeaker`` — a fixed-shape synthetic dataset for the
-  benchmarks (BASELINE configs 3/4: the reference's filelists, wav reading and
-  ``.spec.pt`` caches are outside the hot path).
+  benchmarks (BASELINE configs 3/4).
 """
 from __future__ import annotations
 
+import os
+import random
+
 import torch
+
+from .utils import load_binfn, load_filepaths_and_sid, load_wav_to_torch
+
+
+def _spec_filename(wavfn: str) -> str:
+    return wavfn[:-len(".wav")] + ".spec.pt"
+
+
+class TextAudioSpeakerLoader(torch.utils.data.Dataset):
+    """``data_utils.py:15-102``.  ``spec_device``: when a ``.spec.pt`` cache
+    is missing, compute it with the HIP spectrogram on that device and save it
+    (for ``num_workers=0`` use); without it a missing cache raises and names
+    ``build_spec_cache`` (the reference would fall back to a CPU
+    ``torch.stft`` in the worker)."""
+
+    def __init__(self, filepaths_sid, hparams, spec_device=None):
+        self.filepaths_sid = load_filepaths_and_sid(filepaths_sid)
+        self.sampling_rate = hparams.data.sampling_rate
+        self.filter_length = hparams.data.filter_length
+        self.hop_length = hparams.data.hop_length
+        self.win_length = hparams.data.win_length
+        self.text_channels = hparams.data.text_channels
+        self.segment_size = hparams.train.segment_size
+        self.min_text_len = getattr(hparams.data, "min_text_len", 2)
+        self.max_text_len = getattr(hparams.data, "max_text_len", 384)
+        self.min_wav_len = max(self.segment_size, getattr(hparams.data, "min_wav_len", 0))
+        self.max_wav_len = getattr(hparams.data, "max_wav_len", 10 * self.sampling_rate)
+        self.spec_device = spec_device
+        self._filter()
+        random.seed(1234)
+        random.shuffle(self.filepaths_sid)
+
+    def _filter(self):
+        """Keep ``min_text_len < N < max_text_len`` and ``min_wav_len < L <
+        max_wav_len``; ``lengths`` = L // hop for the bucket sampler
+        (data_utils.py:39-56)."""
+        kept, lengths = [], []
+        for vecfn, wavfn, emofn, sid in self.filepaths_sid:
+            vec = load_binfn(vecfn, self.text_channels)
+            wav, _ = load_wav_to_torch(wavfn)
+            if self.min_text_len < len(vec) < self.max_text_len and \
+                    self.min_wav_len < len(wav) < self.max_wav_len:
+                kept.append([vecfn, wavfn, emofn, sid])
+                lengths.append(len(wav) // self.hop_length)
+        self.filepaths_sid = kept
+        self.lengths = lengths
+
+    def get_item(self, filepaths_sid):
+        vecfn, wavfn, emofn, sid = filepaths_sid
+        return (self.get_text(vecfn), *self.get_audio(wavfn), self.get_emo(emofn),
+                self.get_sid(sid))
+
+    def get_audio(self, filename):
+        audio_norm, sampling_rate = load_wav_to_torch(filename)
+        if sampling_rate != self.sampling_rate:
+            raise ValueError("{} {} SR doesn't match target {} SR".format(
+                filename, sampling_rate, self.sampling_rate))
+        assert len(audio_norm) >= self.segment_size
+        audio_norm = audio_norm.unsqueeze(0)
+        spec_filename = _spec_filename(filename)
+        if os.path.exists(spec_filename):
+            spec = torch.load(spec_filename, weights_only=True)
+        elif self.spec_device is not None:
+            spec = _spectrogram(audio_norm, self, self.spec_device)[0]
+            torch.save(spec, spec_filename)
+        else:
+            raise FileNotFoundError(
+                f"{spec_filename}: no spectrogram cache; run "
+                "vits_amd.data_utils.build_spec_cache(filelist, hps) once before training "
+                "(or pass spec_device= for num_workers=0)")
+        return spec, audio_norm
+
+    def get_text(self, vecfn):
+        return torch.from_numpy(load_binfn(vecfn, self.text_channels))
+
+    def get_emo(self, emofn):
+        return torch.from_numpy(load_binfn(emofn, 1024).flatten())
+
+    def get_sid(self, sid):
+        return torch.LongTensor([int(sid)])
+
+    def __getitem__(self, index):
+        return self.get_item(self.filepaths_sid[index])
+
+    def __len__(self):
+        return len(self.filepaths_sid)
+
+
+def _spectrogram(wavs, hp, device):
+    """[n, L] peak-normalised audio -> [n, F, L // hop] on the HIP STFT
+    (``mel_processing.spectrogram_torch``), returned on the CPU."""
+    from .mel_processing import spectrogram_torch
+
+    y = wavs.to(device=device, dtype=torch.float32)
+    spec = spectrogram_torch(y, hp.filter_length, hp.sampling_rate, hp.hop_length,
+                             hp.win_length, center=False)
+    return spec.cpu()
+
+
+def build_spec_cache(filepaths_sid, hparams, device="cuda", overwrite=False, max_batch=64):
+    """Write the ``.spec.pt`` cache of every utterance of a filelist that
+    lacks one (``data_utils.py:73-81``), on the GPU.  Utterances of equal
+    sample count share one batched HIP STFT launch (up to ``max_batch``).
+    Each file holds the ``[F, T]`` float32 tensor the reference's
+    ``torch.save(spec, ...)`` writes.  Returns the number of files written."""
+    hp = hparams.data
+    todo: dict = {}
+    for _vecfn, wavfn, _emofn, _sid in load_filepaths_and_sid(filepaths_sid):
+        fn = _spec_filename(wavfn)
+        if overwrite or not os.path.exists(fn):
+            wav, sr = load_wav_to_torch(wavfn)
+            if sr != hp.sampling_rate:
+                raise ValueError("{} {} SR doesn't match target {} SR".format(
+                    wavfn, sr, hp.sampling_rate))
+            todo.setdefault(wav.numel(), []).append((fn, wav))
+    written = 0
+    for _n, items in sorted(todo.items()):
+        for i in range(0, len(items), max_batch):
+            chunk = items[i:i + max_batch]
+            spec = _spectrogram(torch.stack([w for _, w in chunk]), hp, device)
+            for (fn, _), s in zip(chunk, spec):
+                torch.save(s.clone(), fn)
+                written += 1
+    return written
 
 
 class DistributedBucketSampler(torch.utils.data.distributed.DistributedSampler):
