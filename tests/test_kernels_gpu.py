@@ -147,6 +147,30 @@ def test_conv1d_presplit_weights_bitwise_equal_f32s(device, monkeypatch, kind, c
     assert torch.equal(outs[True], outs[False])
 
 
+@pytest.mark.parametrize("wdt", [ops.WDT_F32, ops.WDT_F32S])
+def test_conv1d_nonfinite_inputs_stay_nonfinite(device, wdt):
+    """A non-finite activation (the reference's fp32 conv: +-inf or NaN in
+    every output column its receptive field reaches) stays non-finite in
+    exactly those columns on both fp32 paths.  Split fp32 may turn an inf
+    into NaN there (x - hi = inf - inf, engine.FP32_MODE note); finite
+    outputs are unaffected."""
+    g = torch.Generator().manual_seed(11)
+    C, k, T = 128, 7, 300
+    x = torch.randn(2, C, T, generator=g)
+    x[0, 5, 100] = float("inf")
+    x[1, 3, 50] = float("-inf")
+    x[1, 9, 200] = float("nan")
+    w = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
+    ref = F.conv1d(x, w, padding=(k - 1) // 2)
+    with ops.pack_lowp(wdt):
+        layer = ops.pack_conv(w.to(device), None)
+    out = ops.conv1d(x.to(device), layer).cpu()
+    fin = torch.isfinite(ref)
+    assert not fin.all()
+    assert torch.equal(torch.isfinite(out), fin)
+    _close(out[fin], ref[fin], what="finite part")
+
+
 def test_conv1d_masked_split_accumulate(device):
     B, H, T = 3, 64, 150
     g = torch.Generator().manual_seed(3)

@@ -21,8 +21,12 @@ def run(x, layer, n_out, in_slope=1.0, gmask=None, gmask_slope=1.0, io16=False, 
     s.record()
     y = orig_run(x, layer, n_out, in_slope, gmask, gmask_slope, io16, res)
     e.record()
+    # 16-byte staging needs time-contiguous rows, T % 4 == 0, 4-element
+    # aligned strides and base (csrc/conv1d_impl.h launch_tile)
+    v4 = (x.stride(2) == 1 and x.stride(1) % 4 == 0 and x.stride(0) % 4 == 0
+          and x.shape[2] % 4 == 0 and x.data_ptr() % (4 * x.element_size()) == 0)
     key = ("fwd" if gmask is None else "dgrad", layer.m, layer.cin, layer.k, layer.dil, n_out,
-           x.shape[0], layer.tile)
+           x.shape[0], layer.tile, f"v4={int(v4)} tin={x.shape[2]} {tuple(x.stride())}")
     rec[key].append((s, e, 2 * x.shape[0] * layer.m * n_out * layer.cin * layer.k))
     return y
 
@@ -32,7 +36,7 @@ def wgrad(dy, x, k, dil, pad, slope, **kw):
     s.record()
     out = orig_wgrad(dy, x, k, dil, pad, slope, **kw)
     e.record()
-    key = ("wgrad", dy.shape[1], x.shape[1], k, dil, dy.shape[2], x.shape[0], 0)
+    key = ("wgrad", dy.shape[1], x.shape[1], k, dil, dy.shape[2], x.shape[0], 0, "")
     rec[key].append((s, e, 2 * x.shape[0] * dy.shape[1] * dy.shape[2] * x.shape[1] * k))
     return out
 
@@ -56,6 +60,6 @@ for key, v in rec.items():
 tot = sum(r[0] for r in rows)
 print(f"total {tot:.2f} ms over {sum(r[2] for r in rows)} launches")
 for ms, key, n, tf in sorted(rows, reverse=True)[:45]:
-    kind, m, cin, k, dil, n_out, B, tile = key
+    kind, m, cin, k, dil, n_out, B, tile, st = key
     print(f"{ms:7.3f} ms {n:4d}x {tf:7.1f} TF/s  {kind:5s} m={m:4d} cin={cin:4d} k={k:2d} d={dil} "
-          f"T={n_out:6d} B={B:4d} tile={tile}")
+          f"T={n_out:6d} B={B:4d} tile={tile} {st}")

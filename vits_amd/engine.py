@@ -52,7 +52,12 @@ def _param_signature(module: torch.nn.Module):
 # How fp32 models run their convs: "split" (default) = fp32 operands split
 # exactly into three bf16 terms on the bf16 MFMA (VITS_WDT_F32S, fp32-level
 # error, see csrc/conv1d_impl.h split3_bf16), "exact" = the f32-input MFMA
-# (v_mfma_f32_32x32x2_f32, bitwise an fp32 fma chain).
+# (v_mfma_f32_32x32x2_f32, bitwise an fp32 fma chain).  Non-finite
+# activations: split fp32 computes x - hi for an inf x as inf - inf, so an
+# output the reference's fp32 conv gives as +-inf comes out NaN; outputs stay
+# non-finite in exactly the reference's non-finite columns
+# (tests/test_kernels_gpu.py::test_conv1d_nonfinite_inputs_stay_nonfinite).
+# Weights are split on the host with mid = lo = 0 for non-finite values.
 FP32_MODE = os.environ.get("VITS_FP32_MODE", "split")
 if FP32_MODE not in ("split", "exact"):
     raise ValueError(f"VITS_FP32_MODE={FP32_MODE!r}: expected 'split' or 'exact'")

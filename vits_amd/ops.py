@@ -265,7 +265,10 @@ def split_planes(w: torch.Tensor) -> torch.Tensor:
     w = w.to(torch.float32).contiguous()
     mask = torch.tensor(-65536, dtype=torch.int32, device=w.device)
     h = (w.view(torch.int32) & mask).view(torch.float32)
-    r = w - h
+    # (a non-finite weight keeps mid = lo = 0: inf - inf would make them NaN;
+    # a NaN stays NaN in hi even when its payload sits in the truncated bits)
+    h = torch.where(torch.isnan(w), w, h)
+    r = torch.where(torch.isfinite(w), w - h, torch.zeros_like(w))
     m = (r.view(torch.int32) & mask).view(torch.float32)
     lo = r - m
     return torch.stack([h, m, lo], dim=-3).to(torch.bfloat16)
