@@ -161,3 +161,35 @@ def test_mwsd_gpu_fp16_autocast_vs_reference(device, monkeypatch):
     print("torch f16:", ref16)
     for k in hip:
         assert hip[k] <= 2.0 * ref16[k] + 1e-3, (k, hip[k], ref16[k])
+
+
+@pytest.mark.parametrize("C,F,T,k0,s0,slope", [(1, 65, 19, 5, 2, 1.0), (64, 61, 37, 5, 2, 0.2),
+                                               (64, 7, 23, 7, 1, 0.2), (3, 30, 9, 3, 3, 0.2)])
+def test_conv2d_freq_joined_rows_layout_cpu(monkeypatch, C, F, T, k0, s0, slope):
+    """The STFT-discriminator lowering (discriminators.conv2d_freq: frequency
+    windows unfolded into channels, the F_out rows joined along time with
+    their own zero padding) restated on the CPU: the HIP training conv is
+    swapped for torch conv1d (with the leaky-relu prologue), so this checks
+    only the unfold / join / slice index math against torch conv2d, fp64."""
+    import torch.nn.functional as F_
+
+    import vits_amd.discriminators as D
+
+    def conv1d_hip(x, w, bias, dilation, padding, in_slope, wdt, residual=None):
+        xa = F_.leaky_relu(x, in_slope) if in_slope != 1.0 else x
+        return F_.conv1d(xa, w.to(x.dtype), None if bias is None else bias.to(x.dtype),
+                         padding=padding, dilation=dilation)
+
+    monkeypatch.setattr(D.train_ops, "conv1d_hip", conv1d_hip)
+    g = torch.Generator().manual_seed(C + F + T)
+    layer = torch.nn.Conv2d(C, 16, (k0, 5), stride=(s0, 1), padding=(0, 2)).double()
+    x = torch.randn(2, C, F, T, generator=g, dtype=torch.float64, requires_grad=True)
+    y = D.conv2d_freq(layer, x, None, in_slope=slope)
+    xa = F_.leaky_relu(x, slope) if slope != 1.0 else x
+    ref = F_.conv2d(xa, layer.weight, layer.bias, stride=(s0, 1), padding=(0, 2))
+    assert y.shape == ref.shape
+    assert torch.allclose(y, ref, atol=1e-12, rtol=1e-12)
+    dy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    gx, gw = torch.autograd.grad(y, (x, layer.weight), dy)
+    rx, rw = torch.autograd.grad(ref, (x, layer.weight), dy)
+    assert torch.allclose(gx, rx, atol=1e-12) and torch.allclose(gw, rw, atol=1e-10)

@@ -287,13 +287,15 @@ def test_conv_transpose1d_train_polyphase(device, C, O, K, u, T):
     _close(md.bias.grad, (_r16(dy) if train_ops.TRAIN_IO16 else dy).sum((0, 2)), "db")
 
 
-@pytest.mark.parametrize("C,F,T,k0,s0", [(1, 65, 289, 5, 2), (1, 1025, 19, 5, 2),
-                                         (64, 31, 145, 5, 2), (1, 257, 73, 7, 3)])
-def test_conv2d_freq_unfolded(device, C, F, T, k0, s0):
+@pytest.mark.parametrize("C,F,T,k0,s0,slope", [(1, 65, 289, 5, 2, 1.0), (1, 1025, 19, 5, 2, 1.0),
+                                               (64, 31, 145, 5, 2, 1.0), (1, 257, 73, 7, 3, 1.0),
+                                               (64, 61, 19, 5, 2, 0.2), (64, 13, 37, 5, 2, 0.2)])
+def test_conv2d_freq_unfolded(device, C, F, T, k0, s0, slope):
     """STFT-discriminator Conv2d(C, 64, (k0, 5), stride (s0, 1), padding (0, 2))
-    as the unfolded stride-1 Conv1d on the HIP training conv
-    (discriminators.conv2d_freq): output, magnitude gradient, weight and bias
-    gradients vs torch conv2d in fp32 on the same fp16-rounded operands."""
+    (after leaky_relu(slope)) as the unfolded, row-joined stride-1 Conv1d on
+    the HIP training conv (discriminators.conv2d_freq): output, magnitude
+    gradient, weight and bias gradients vs torch conv2d in fp32 on the same
+    fp16-rounded operands."""
     import vits_amd.discriminators as D
 
     g = torch.Generator().manual_seed(C * 1000 + F + k0)
@@ -306,12 +308,16 @@ def test_conv2d_freq_unfolded(device, C, F, T, k0, s0):
     dy = torch.randn(2, 64, F_out, T, generator=g)
     ld = layer.to(device)
     xd = x.to(device).requires_grad_(True)
-    y = D.conv2d_freq(ld, xd, train_ops.TRAIN_WDTYPE)
+    if slope != 1.0:
+        x = x - 0.5  # (both signs through the leaky relu)
+        xd = x.to(device).requires_grad_(True)
+    y = D.conv2d_freq(ld, xd, train_ops.TRAIN_WDTYPE, in_slope=slope)
     y.backward(dy.to(device).to(y.dtype))
     wr = _r16(layer.weight.detach().cpu()).requires_grad_(True)
     br = layer.bias.detach().cpu().clone().requires_grad_(True)
     xr = _r16(x).requires_grad_(True)
-    yr = F_.conv2d(xr, wr, br, stride=(s0, 1), padding=(0, 2))
+    xa = F_.leaky_relu(xr, slope) if slope != 1.0 else xr
+    yr = F_.conv2d(_r16(xa) if slope != 1.0 else xa, wr, br, stride=(s0, 1), padding=(0, 2))
     yr.backward(_r16(dy))
     _close(y, yr, "y", tol=TOL_Y)
     _close(xd.grad, xr.grad, "dx", tol=TOL_Y)

@@ -115,6 +115,19 @@ class STFTDiscriminator(nn.Module):
             # conv kernel in the step) on the HIP training conv
             h = conv2d_freq(first, h, wdt)
             layers = layers[1:]
+        if STFT_D_HIP_ALL and wdt is not None and layers and all(
+                _freq_conv_ok(l) for l in layers if isinstance(l, Conv2d)):
+            # every remaining layer on the HIP training conv, the LeakyReLU
+            # between two layers fused into the next conv's input staging
+            # (and its derivative into that conv's data-gradient epilogue)
+            slope = 1.0
+            for layer in layers:
+                if isinstance(layer, LeakyReLU):
+                    slope = layer.negative_slope
+                else:
+                    h = conv2d_freq(layer, h, wdt, in_slope=slope)
+                    slope = 1.0
+            return h.squeeze(1).squeeze(2)
         if STFT_D_NHWC and h.device.type == "cuda":
             h = h.contiguous(memory_format=torch.channels_last)
             for layer in layers:
@@ -131,6 +144,8 @@ class STFTDiscriminator(nn.Module):
 
 
 STFT_D_HIP = True  # test switch: False keeps every STFT-discriminator conv on torch
+# all STFT-discriminator layers (not only the first) on the HIP conv
+STFT_D_HIP_ALL = os.environ.get("VITS_STFT_D_HIP_ALL", "0") != "0"
 # channels-last operands for the STFT discriminators' MIOpen convs: its NHWC
 # solvers then run without the NCHW<->NHWC batched transposes around every
 # conv (train step 104.1 -> 101.3 ms); VITS_STFT_D_NHWC=0 restores NCHW
@@ -144,24 +159,35 @@ def _freq_conv_ok(layer) -> bool:
             and train_ops._lib_k_ok(layer.kernel_size[1], 1))
 
 
-def conv2d_freq(layer, h, wdt):
+def conv2d_freq(layer, h, wdt, in_slope: float = 1.0):
     """Conv2d(C, O, (k0, k1), stride (s0, 1), padding (0, p1)) over [B, C, F, T]
-    as ONE stride-1 Conv1d along time: the frequency windows are unfolded
-    into channels ([B * F_out, C * k0, T]) and the weight [O, C, k0, k1] is
-    read as [O, C * k0, k1].  Forward, data and weight gradient run on the
-    HIP training conv (Conv1dHip); the unfold's backward folds the data
-    gradient back onto the frequency axis.  Returns [B, O, F_out, T] (a
-    permuted view)."""
+    (after leaky_relu(., in_slope) when in_slope != 1) as ONE stride-1 Conv1d
+    along time: the frequency windows are unfolded into channels and the F_out
+    rows joined along time ([B, C * k0, F_out * (T + 2 p1)]), the weight
+    [O, C, k0, k1] is read as [O, C * k0, k1].  Forward, data and weight
+    gradient run on the HIP training conv (Conv1dHip16, the leaky-relu as its
+    input prologue); the unfold's backward folds the data gradient back onto
+    the frequency axis.  Returns [B, O, F_out, T] (a strided view)."""
     B, C, F_, T = h.shape
     O = layer.out_channels
     k0, k1 = layer.kernel_size
     s0 = layer.stride[0]
+    p1 = layer.padding[1]
     F_out = (F_ - k0) // s0 + 1
-    u = h.unfold(2, k0, s0)                                    # [B, C, F_out, T, k0]
-    u = u.permute(0, 2, 1, 4, 3).reshape(B * F_out, C * k0, T)
+    # The F_out frequency rows of an utterance lie end to end along the time
+    # axis, each framed by its own p1 zero columns (L = T + 2 p1 per row), so
+    # the conv runs over [B, C*k0, F_out*L]: long time rows for the MFMA
+    # tiles instead of B*F_out "utterances" of T = 19..289 frames (a 256-
+    # column tile was 7-30 % occupied; the unfolded layer and its data
+    # gradient took ~8 ms of a B=32 step).  With padding p1 on the joined
+    # axis, output column f*L + p1 + t reads row f's columns t-p1 .. t+p1 only.
+    L = T + 2 * p1
+    hp = torch.nn.functional.pad(h, (p1, p1))                   # [B, C, F, L]
+    u = hp.unfold(2, k0, s0)                                    # [B, C, F_out, L, k0]
+    u = u.permute(0, 1, 4, 2, 3).reshape(B, C * k0, F_out * L)
     w = layer.weight.reshape(O, C * k0, k1)
-    y = train_ops.conv1d_hip(u, w, layer.bias, 1, layer.padding[1], 1.0, wdt)
-    return y.view(B, F_out, O, y.shape[2]).permute(0, 2, 1, 3)
+    y = train_ops.conv1d_hip(u, w, layer.bias, 1, p1, in_slope, wdt)  # [B, O, F_out*L]
+    return y.view(B, O, F_out, L)[..., p1:p1 + T]
 
 
 class MultiSTFTDiscriminator(nn.Module):
@@ -208,7 +234,8 @@ class GroupedSpectralNorm:
         # first, which conv2d_freq lowers onto the HIP conv): their W / sigma
         # is produced as the fp16 channels-last operand under autocast
         firsts = {id(sub.convs[0]) for sub in root.modules() if isinstance(sub, STFTDiscriminator)}
-        cl = STFT_D_NHWC and os.environ.get("VITS_SN_CL", "1") != "0"  # A/B switch
+        cl = (STFT_D_NHWC and not STFT_D_HIP_ALL
+              and os.environ.get("VITS_SN_CL", "1") != "0")  # A/B switch
         self.cl16 = [cl and isinstance(m, Conv2d) and id(m) not in firsts for m, _, _ in self.flat]
 
     def _fused_ok(self) -> bool:
