@@ -181,8 +181,11 @@ def conv2d_freq(layer, h, wdt, in_slope: float = 1.0):
     # column tile was 7-30 % occupied; the unfolded layer and its data
     # gradient took ~8 ms of a B=32 step).  With padding p1 on the joined
     # axis, output column f*L + p1 + t reads row f's columns t-p1 .. t+p1 only.
-    L = T + 2 * p1
-    hp = torch.nn.functional.pad(h, (p1, p1))                   # [B, C, F, L]
+    # (L rounded up to a multiple of 4: time-contiguous rows of whole 4-step
+    # blocks, the conv kernels' 16-byte staging path; the extra columns are
+    # zeros on the right of each row)
+    L = (T + 2 * p1 + 3) // 4 * 4
+    hp = torch.nn.functional.pad(h, (p1, L - T - p1))           # [B, C, F, L]
     u = hp.unfold(2, k0, s0)                                    # [B, C, F_out, L, k0]
     u = u.permute(0, 1, 4, 2, 3).reshape(B, C * k0, F_out * L)
     w = layer.weight.reshape(O, C * k0, k1)

@@ -244,6 +244,12 @@ F32P_MAX_KC = int(os.environ.get("VITS_F32P_KC", "32"))
 
 
 def _kc_f32p(cin_pad: int, k: int, dil: int, tile: int) -> int:
+    if tile == TILE_64x128:
+        # 64-row layers (the 64-channel decoder stage): 16-channel chunks halve
+        # the double-buffered window (3 instead of 2 workgroups per CU);
+        # measured on MI355X (tools/conv_bench.py WDT=3, r03): c1 k=3/7/11
+        # +15/+8/+3 %, c2 +12..17 % over 32-channel chunks
+        return 16
     bn = TILE_COLS[tile]
     xrs = (bn + (k - 1) * dil + 3 + 3) // 4 * 4  # window row incl. the 16-byte alignment shift
     budget = 6144 if bn <= 128 else 10240

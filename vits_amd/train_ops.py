@@ -457,11 +457,12 @@ def wn_update(x: torch.Tensor, rs: torch.Tensor, mask: torch.Tensor, out):
     out / mask and a 16-bit rs; None otherwise (the caller runs torch)."""
     wdt = autocast_wdtype() if x.device.type == "cuda" else None
     if (wdt is None or not _io16(wdt) or rs.dtype != _TORCH_16[wdt] or x.dtype != torch.float32
-            or mask.dtype != torch.float32 or not x.is_contiguous() or not rs.is_contiguous()
-            or not mask.is_contiguous() or (out is not None and (out.dtype != torch.float32
-                                                                 or not out.is_contiguous()))):
+            or mask.dtype != torch.float32 or (out is not None and out.dtype != torch.float32)):
         return None
-    return WNUpdate16.apply(x, rs, mask, out, wdt)
+    # (a strided x - the PosteriorEncoder's pre-conv output - is copied once
+    # here; the fused update's outputs are contiguous from then on)
+    return WNUpdate16.apply(x.contiguous(), rs.contiguous(), mask.contiguous(),
+                            None if out is None else out.contiguous(), wdt)
 
 
 # 16-bit activations for the training convs / gates under fp16 autocast (the
