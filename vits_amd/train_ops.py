@@ -564,8 +564,21 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0,
             x = F.leaky_relu(x, in_slope)
         return module(x) if residual is None else module(x) + residual
     w = weight_norm_effective(module)
+    if (GEMM_1X1_MAX_T and w.shape[2] == 1 and module.padding[0] == 0 and in_slope == 1.0
+            and residual is None and x.shape[2] <= GEMM_1X1_MAX_T and _io16(wdt)):
+        # a 1x1 conv on a short time axis (the text encoder's q/k/v/o and
+        # FFN projections, T = 100) is a plain batched GEMM: hipBLASLt via
+        # torch.matmul under autocast (the tiled conv kernel leaves most of a
+        # 128-column tile and most CUs idle at B*ceil(T/128) workgroups)
+        t16 = _TORCH_16[wdt]
+        y = torch.matmul(w[:, :, 0].to(t16), x.to(t16))
+        return y if module.bias is None else y + module.bias.to(t16)[:, None]
     return conv1d_hip(x, w, module.bias, module.dilation[0], module.padding[0], in_slope, wdt,
                       residual)
+
+
+# 1x1 training convs with T <= this run as hipBLASLt GEMMs (0: always the HIP conv)
+GEMM_1X1_MAX_T = int(os.environ.get("VITS_TRAIN_GEMM1X1", "0"))
 
 
 # ---------------------------------------------------------------------------
