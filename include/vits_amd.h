@@ -326,6 +326,15 @@ int vits_layer_norm_channels(const float* x, const float* r, const float* gamma,
                              int64_t post_add_bstride, float scale, const float* pos,
                              const float* pos_alpha, void* stream);
 
+/* backward of y = LN(x) * gamma + beta (training; gamma optional):        */
+/*   dx [B][C][T]; dgamma_part / dbeta_part (optional) [B * ceil(T/64)][C] */
+/*   per-tile partial sums the caller reduces over rows.                   */
+/*   Replaces the autograd of modules.LayerNorm (modules.py:41-44).        */
+int vits_layer_norm_channels_backward(const float* x, const float* gamma, const float* dy,
+                                      float* dx, float* dgamma_part, float* dbeta_part,
+                                      int batch, int channels, int t_len, float eps,
+                                      void* stream);
+
 /* ---------------------------------------------------------------------- */
 /* scaled-dot-product attention over [B][H*D][T] channel-major q/k/v      */
 /* (batch stride qkv_bstride, e.g. slices of one fused q|k|v buffer), key */

@@ -393,3 +393,34 @@ def test_wn_update_matches_torch(with_out):
     for i, (g, w) in enumerate(zip(got, want)):
         assert g.dtype == w.dtype and g.shape == w.shape, i
         assert torch.equal(g, w), (i, (g.float() - w.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("B,C,T", [(2, 192, 100), (3, 96, 37), (1, 256, 500)])
+def test_layer_norm_hip_fwd_bwd(device, monkeypatch, B, C, T):
+    """modules.LayerNorm on the GPU (train_ops.LayerNormHip: HIP forward and
+    backward over the channel axis) vs the reference's transpose +
+    F.layer_norm (modules.py:41-44) in fp64 on the CPU: y, dx, dgamma, dbeta."""
+    from vits_amd import modules
+
+    monkeypatch.setattr(train_ops, "LN_HIP", True)
+    g = torch.Generator().manual_seed(B * C + T)
+    x = torch.randn(B, C, T, generator=g) * 2 + 0.5
+    dy = torch.randn(B, C, T, generator=g)
+    ln = modules.LayerNorm(C)
+    with torch.no_grad():
+        ln.gamma.copy_(torch.randn(C, generator=g))
+        ln.beta.copy_(torch.randn(C, generator=g))
+    xr = x.double().requires_grad_(True)
+    gr = ln.gamma.detach().double().requires_grad_(True)
+    br = ln.beta.detach().double().requires_grad_(True)
+    yr = F_.layer_norm(xr.transpose(1, -1), (C,), gr, br, 1e-5).transpose(1, -1)
+    yr.backward(dy.double())
+    ld = ln.to(device)
+    xd = x.to(device).requires_grad_(True)
+    y = ld(xd)
+    y.backward(dy.to(device))
+    for got, ref, what in ((y, yr, "y"), (xd.grad, xr.grad, "dx"), (ld.gamma.grad, gr.grad, "dgamma"),
+                           (ld.beta.grad, br.grad, "dbeta")):
+        got = got.detach().double().cpu()
+        err = (got - ref.detach()).abs().max().item() / ref.detach().abs().max().item()
+        assert err < 2e-5, (what, err)

@@ -276,6 +276,10 @@ _SIGS = {
         + [C.c_float, C.c_void_p, C.c_void_p, C.c_int64, C.c_float, C.c_void_p, C.c_void_p,
            C.c_void_p],
     ),
+    "vits_layer_norm_channels_backward": (
+        C.c_int,
+        [C.c_void_p] * 6 + [C.c_int] * 3 + [C.c_float, C.c_void_p],
+    ),
     "vits_attention_forward": (
         C.c_int,
         [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p],

@@ -856,6 +856,26 @@ def layer_norm_channels(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Op
     return out
 
 
+def layer_norm_channels_backward(x: torch.Tensor, gamma: Optional[torch.Tensor], dy: torch.Tensor,
+                                 eps: float = 1e-5, need_affine: bool = True):
+    """(dx, dgamma, dbeta) of y = LN_C(x) * gamma + beta on [B, C, T] fp32
+    contiguous x / dy (vits_layer_norm_channels_backward); dgamma / dbeta
+    None when not need_affine."""
+    require_device(x, gamma, dy)
+    assert x.is_contiguous() and dy.is_contiguous() and x.shape == dy.shape
+    B, Cc, T = x.shape
+    dx = torch.empty_like(x)
+    rows = B * ((T + 63) // 64)
+    dgp = torch.empty(rows, Cc, device=x.device) if need_affine else None
+    dbp = torch.empty(rows, Cc, device=x.device) if need_affine else None
+    check(_lib.load().vits_layer_norm_channels_backward(
+        x.data_ptr(), _ptr(gamma), dy.data_ptr(), dx.data_ptr(), _ptr(dgp), _ptr(dbp), B, Cc, T,
+        eps, _stream_ptr(x.device)), "vits_layer_norm_channels_backward")
+    if not need_affine:
+        return dx, None, None
+    return dx, dgp.sum(0), dbp.sum(0)
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, n_heads: int,
               lengths: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
     """softmax((q/sqrt(d)) k^T, masked -1e4) v on [B, H*D, T] channel-major tensors."""

@@ -42,7 +42,8 @@ from . import _lib
 from ._lib import (EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128, WDT_BF16,
                    WDT_F16, ConvWgradDesc, check)
 from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
-                  make_desc, make_out, weight_norm_effective)
+                  layer_norm_channels, layer_norm_channels_backward, make_desc, make_out,
+                  weight_norm_effective)
 
 _TORCH_16 = {WDT_F16: torch.float16, WDT_BF16: torch.bfloat16}
 TRAIN_WDTYPE = WDT_F16  # the reference's autocast dtype (train_stft.py:165)
@@ -372,6 +373,42 @@ class Conv1dHip16(torch.autograd.Function):
             return dx, dw, db, None, None, None, None
         dres = dy if ctx.needs_input_grad[7] else None
         return dx, dw, db, None, None, None, None, dres
+
+
+# modules.LayerNorm on the HIP kernels on the GPU (VITS_LN_HIP=1).  Off by
+# default: measured 78.4 vs 77.4 ms per B=32 train step against torch's
+# layer_norm (the per-channel wave reductions of dgamma / dbeta and the
+# (utterance, 64-frame) grid - 256 workgroups at T=500 - lose to it)
+LN_HIP = os.environ.get("VITS_LN_HIP", "0") != "0"
+
+
+class LayerNormHip(torch.autograd.Function):
+    """modules.LayerNorm (modules.py:33-44) on the GPU: y = LN over C of
+    [B, C, T] * gamma + beta in fp32 (the reference's F.layer_norm, which
+    autocast runs in fp32, on a transposed view), forward
+    vits_layer_norm_channels, backward vits_layer_norm_channels_backward
+    (dx, and dgamma / dbeta from per-tile partial sums)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps: float):
+        x32 = x.detach().float().contiguous()
+        g = gamma.detach().float().contiguous()
+        b = beta.detach().float().contiguous()
+        y = layer_norm_channels(x32, g, b, eps)
+        ctx.save_for_backward(x32, g)
+        ctx.eps = eps
+        ctx.xdtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x32, g = ctx.saved_tensors
+        need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dx, dg, db = layer_norm_channels_backward(x32, g, dy.float().contiguous(), ctx.eps,
+                                                  need_affine)
+        return (dx.to(ctx.xdtype) if ctx.needs_input_grad[0] else None,
+                dg if ctx.needs_input_grad[1] else None,
+                db if ctx.needs_input_grad[2] else None, None)
 
 
 class GateHip16(torch.autograd.Function):
