@@ -205,9 +205,15 @@ int vits_expand_prior(const float* attn, const float* m, const float* s, const f
 /*   z[b][c][t] = m[b][c][x(t)] + noise(c,t) * s[b][c][x(t)] * noise_scale  */
 /*   for t < y_len (x(t): cum[x-1] <= t < cum[x]), 0 for y_len <= t < t_y;  */
 /*   lens[i][b] = y_len * stage_mult[i].  noise_mode 0: noise [B][C][t_y];  */
-/*   1: element (c, t) at noise[s + c*y_len + t], s = noise_start[b] mod    */
-/*   (noise_len - C*y_len) (EmoVITS's buffer slice at a random start,      */
-/*   infer.py:172-175).  t_x <= 4096, n_stage <= 8.                         */
+/*   1: element (c, t) at noise[s + c*y_len + t] (EmoVITS's buffer slice,   */
+/*   infer.py:172-175), s = np.random.randint(noise_len - C*y_len) drawn on */
+/*   the device exactly as numpy's legacy RandomState does (masked         */
+/*   rejection) from noise_start = [B][VITS_ED_DRAWS] raw MT19937 uint32    */
+/*   words; lens must then have n_stage + 1 rows: lens[n_stage][b] = words  */
+/*   consumed (the host re-advances its generator by that many), or -1 when */
+/*   the slice does not fit (the reference's randint raises; z = 0, no     */
+/*   noise read).  t_x <= 4096, n_stage <= 8.                               */
+#define VITS_ED_DRAWS 32
 /* ---------------------------------------------------------------------- */
 int vits_expand_durations(const float* logw, int64_t logw_bstride, const int32_t* x_len, int t_x,
                           float rate, int half_round, const float* m, const float* s,

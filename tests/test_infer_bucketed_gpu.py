@@ -10,6 +10,8 @@ bucket with every conv masked at y_len (and tiles past y_len + 64 skipped),
 so each output sample is computed by the same kernels with the same
 summation order as the exact-length eager run: the comparisons are
 BITWISE (torch.equal on the first y_len * hop samples)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -76,9 +78,10 @@ def test_infer_bucketed_graph_replay_and_padded_text(base, device):
 
 def test_emovits_graph_mode_equals_eager_mode(device, tmp_path):
     """EmoVITS (fp16 model, noise slices of its fixed buffer) in graph mode
-    (one replay per utterance) vs its eager mode on the same noise slice:
-    bitwise equal waveforms.  The device folds a raw start draw into the
-    valid range; the eager run is given the same folded start."""
+    (one replay per utterance) vs its eager mode from the same numpy seed:
+    bitwise equal waveforms, and numpy's generator ends in the same state
+    (the device draws infer.py:173's randint(len - nl) from raw words of
+    numpy's own generator, as numpy's legacy masked rejection does)."""
     from vits_amd.infer import EmoVITS
     from vits_amd.utils import get_hparams_from_dict
 
@@ -93,30 +96,38 @@ def test_emovits_graph_mode_equals_eager_mode(device, tmp_path):
     x, emo, sid, _ = _inputs(device, 41, 5)
     text = x[0].float().cpu().numpy()
     emo_h = emo.half()
-    raw = 123456789
-    np.random.seed(0)
-    orig = np.random.randint
-    np.random.randint = lambda *a, **k: raw
-    try:
-        wav_g, _ = ev.infer(int(sid), text, emo_h)
-    finally:
-        np.random.randint = orig
-    # eager with the folded start of the device
-    m = ev.model
-    text_t = torch.from_numpy(text).half().to(device).unsqueeze(0)
-    m_p, s_p, logw, gg = m.infer_p1(text_t, emo_h, sid)
-    w_ceil = torch.ceil(torch.exp(logw) * 1.0)
-    y_len = int(torch.clamp_min(torch.sum(w_ceil), 1).item())
-    nl = 192 * y_len
-    start = raw % (ev.noise.numel() - nl)
-    from vits_amd.commons import infer_path
+    outs = []
+    for graph in (True, False):
+        ev.graph = graph
+        for seed in (0, 11):
+            np.random.seed(seed)
+            wav, _ = ev.infer(int(sid), text, emo_h)
+            outs.append((wav, np.random.randint(1 << 30)))
+    for (wg, ng), (we, ne) in zip(outs[:2], outs[2:]):
+        assert wg.shape == we.shape and np.isfinite(wg).all()
+        assert np.array_equal(wg, we)
+        assert ng == ne
+    assert not np.array_equal(outs[0][0], outs[1][0])  # different seeds, different slices
 
-    noise = ev.noise[start:start + nl].view(1, 192, y_len)
-    attn = infer_path(w_ceil.float(), 41, y_len).half()
-    ref = m.infer_p2(attn, m_p, s_p, gg, noise).float().view(-1).cpu().numpy()
-    assert wav_g.shape == ref.shape == (y_len * 192,)
-    assert np.array_equal(wav_g, ref)
-    # eager mode of the wrapper itself agrees on shape / finiteness
-    ev.graph = False
-    wav_e, _ = ev.infer(int(sid), text, emo_h)
-    assert wav_e.shape == ref.shape and np.isfinite(wav_e).all()
+
+@pytest.mark.gpu
+def test_expand_durations_noise_slice_overflow_reads_nothing(device):
+    """A y_len whose slice does not fit the flat noise buffer (C * y_len >
+    numel; the reference's randint raises) writes z = 0 and flags -1 in the
+    extra lens row instead of reading past the buffer."""
+    from vits_amd import ops
+
+    B, C, t_x, t_y = 2, 8, 6, 64
+    logw = torch.full((B, 1, t_x), math.log(8.0), device=device)  # 48 frames each
+    logw[1] = math.log(2.0)                                        # 12 frames
+    m_p = torch.randn(B, C, t_x, device=device)
+    s_p = torch.rand(B, C, t_x, device=device)
+    noise = torch.randn(C * 40, device=device)  # room for 40 frames only
+    pool = torch.from_numpy(np.stack([ops.numpy_draw_pool()[0] for _ in range(B)])).to(device)
+    z, lens = ops.expand_durations(logw, m_p, s_p, noise, t_y, noise_start=pool,
+                                   stage_mult=(1, 2))
+    lens = lens.cpu()
+    assert lens[0].tolist() == [48, 12] and lens[1].tolist() == [96, 24]
+    assert int(lens[2, 0]) == -1 and int(lens[2, 1]) >= 1
+    assert torch.count_nonzero(z[0]).item() == 0
+    assert torch.count_nonzero(z[1, :, :12]).item() == C * 12

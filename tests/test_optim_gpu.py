@@ -106,6 +106,27 @@ def test_fused_radam_resume_continues_step(device, tmp_path):
     assert float(oc.state[pc[0]]["step"]) == 6.0
 
 
+def test_fused_radam_state_dict_leaves_live_counter(device):
+    """state_dict() must not freeze the live step: save after 2
+    steps, step 3 more, save again -> the second checkpoint holds step 5 and
+    the live state still points at the device counter."""
+    shapes = _shapes()
+    params, grads = _seq(shapes, 5, 2)
+    pa = [p.to(device).requires_grad_(True) for p in params]
+    oa = FusedRAdam(pa, 1e-4)
+    for i, gs in enumerate(grads):
+        for p, g in zip(pa, gs):
+            p.grad = g.to(device)
+        oa.step()
+        if i == 1:
+            sd1 = oa.state_dict()
+    sd2 = oa.state_dict()
+    assert all(st["step"] == 2 for st in sd1["state"].values())
+    assert all(st["step"] == 5 for st in sd2["state"].values())
+    assert isinstance(oa.state[pa[0]]["step"], torch.Tensor)
+    assert float(oa.state[pa[0]]["step"]) == 5.0
+
+
 def test_fused_radam_loads_reference_int_step_state(device):
     """A reference D_*.pth holds radam.py's per-parameter int ``step``
     (radam.py:55): loaded into FusedRAdam it seeds the device counter."""

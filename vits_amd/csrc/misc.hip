@@ -142,6 +142,7 @@ __global__ __launch_bounds__(256) void expand_prior_kernel(const float* __restri
 constexpr int ED_T = 64;
 constexpr int ED_MAX_TX = 4096;
 constexpr int ED_MAX_STAGES = 8;
+constexpr int ED_DRAWS = VITS_ED_DRAWS;  // raw generator words per utterance (mode 1)
 struct EdStages {
   int32_t mult[ED_MAX_STAGES];
   int n;
@@ -219,12 +220,42 @@ __global__ __launch_bounds__(256) void expand_durations_kernel(
   // 3) z[b][c][t] = m[c][x] + (noise(c, t) * s[c][x]) * noise_scale, 0 past y_len
   const float* mb = m + (int64_t)b * ms_bstride;
   const float* sb = s + (int64_t)b * ms_bstride;
-  // mode 1: the slice start (infer.py:173 draws randint(len - C*y_len)); a
-  // raw draw is folded into [0, noise_len - C*y_len) here, where y_len is known
+  // mode 1: the slice start of infer.py:173, np.random.randint(noise_len -
+  // C*y_len), drawn here where y_len is known, exactly as numpy's legacy
+  // RandomState draws it: rng = high - 1; rng == 0 -> 0 without a draw;
+  // else the first raw MT19937 word u of the pool with (u & mask) <= rng,
+  // mask = the smallest 2^k - 1 >= rng (numpy's masked rejection for ranges
+  // below 2^32).  The number of words consumed goes to lens[n_stage][b] so
+  // the host re-advances its generator by exactly that many; -1 when the
+  // slice does not fit (the reference's randint raises) or the pool ran out:
+  // z is then all zeros and no noise element is read.
   int64_t nbase = 0;
+  bool noise_ok = true;
   if (noise_mode) {
-    const int64_t room = noise_len - (int64_t)channels * y_len;
-    nbase = noise_start ? (int64_t)noise_start[b] % (room > 1 ? room : 1) : 0;
+    const int64_t high = noise_len - (int64_t)channels * y_len;
+    int used = -1;
+    if (high >= 1 && high - 1 <= 0xFFFFFFFFll) {
+      const uint32_t rng = (uint32_t)(high - 1);
+      if (rng == 0) {
+        used = 0;
+      } else {
+        uint32_t mask = rng;
+        mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+        mask |= mask >> 8; mask |= mask >> 16;
+        const uint32_t* pool = reinterpret_cast<const uint32_t*>(noise_start) +
+                               (int64_t)b * ED_DRAWS;
+        for (int i = 0; i < ED_DRAWS; ++i) {
+          const uint32_t u = pool[i] & mask;
+          if (u <= rng) {
+            nbase = u;
+            used = i + 1;
+            break;
+          }
+        }
+      }
+    }
+    noise_ok = used >= 0;
+    if (blockIdx.x == 0 && tid == 0) lens[st.n * batch + b] = used;
   }
   for (int i = tid; i < channels * ED_T; i += 256) {
     const int c = i / ED_T;
@@ -233,7 +264,7 @@ __global__ __launch_bounds__(256) void expand_durations_kernel(
     if (t >= t_y) continue;
     const int x = xi[tl];
     float v = 0.f;
-    if (x >= 0) {
+    if (x >= 0 && noise_ok) {
       // mode 0: noise [B][C][t_y]; mode 1: EmoVITS's buffer slice viewed as
       // [C][y_len] from element noise_start[b] (infer.py:172-175)
       const float n = noise_mode ? noise[nbase + (int64_t)c * y_len + t]
@@ -346,6 +377,7 @@ extern "C" int vits_expand_durations(const float* logw, int64_t logw_bstride,
                  t_x > 0);
   VITS_CHECK_ARG(n_stage >= 1 && n_stage <= ED_MAX_STAGES && (n_stage == 1 || stage_mult));
   VITS_CHECK_SHAPE(t_x <= ED_MAX_TX && ms_cstride >= t_x);
+  VITS_CHECK_ARG(noise_mode == 0 || (noise_mode == 1 && noise_start));
   EdStages st;
   st.n = n_stage;
   for (int i = 0; i < ED_MAX_STAGES; ++i) st.mult[i] = i < n_stage ? (stage_mult ? stage_mult[i] : 1) : 0;

@@ -131,22 +131,31 @@ def build_spec_cache(filepaths_sid, hparams, device="cuda", overwrite=False, max
     lacks one (``data_utils.py:73-81``), on the GPU.  Utterances of equal
     sample count share one batched HIP STFT launch (up to ``max_batch``).
     Each file holds the ``[F, T]`` float32 tensor the reference's
-    ``torch.save(spec, ...)`` writes.  Returns the number of files written."""
+    ``torch.save(spec, ...)`` writes.  The first pass reads only each WAV's
+    header (sample rate, sample count; the data is memory-mapped, not
+    loaded); audio is loaded ``max_batch`` utterances at a time in the
+    compute loop, so host memory stays bounded by one batch whatever the
+    dataset size.  Returns the number of files written."""
+    from scipy.io import wavfile
+
     hp = hparams.data
     todo: dict = {}
     for _vecfn, wavfn, _emofn, _sid in load_filepaths_and_sid(filepaths_sid):
         fn = _spec_filename(wavfn)
         if overwrite or not os.path.exists(fn):
-            wav, sr = load_wav_to_torch(wavfn)
+            sr, data = wavfile.read(wavfn, mmap=True)
             if sr != hp.sampling_rate:
                 raise ValueError("{} {} SR doesn't match target {} SR".format(
                     wavfn, sr, hp.sampling_rate))
-            todo.setdefault(wav.numel(), []).append((fn, wav))
+            todo.setdefault(int(data.size), []).append((fn, wavfn))
+            del data
     written = 0
     for _n, items in sorted(todo.items()):
         for i in range(0, len(items), max_batch):
             chunk = items[i:i + max_batch]
-            spec = _spectrogram(torch.stack([w for _, w in chunk]), hp, device)
+            wavs = torch.stack([load_wav_to_torch(w)[0] for _, w in chunk])
+            spec = _spectrogram(wavs, hp, device)
+            del wavs
             for (fn, _), s in zip(chunk, spec):
                 torch.save(s.clone(), fn)
                 written += 1

@@ -155,6 +155,9 @@ STFT_D_NHWC = os.environ.get("VITS_STFT_D_NHWC", "1") != "0"
 def _freq_conv_ok(layer) -> bool:
     return (isinstance(layer, Conv2d) and layer.groups == 1 and layer.dilation == (1, 1)
             and layer.stride[1] == 1 and layer.padding[0] == 0
+            # joined rows are sliced at [p1, p1 + T]: only a 'same' time conv
+            # reads nothing but its own row
+            and 2 * layer.padding[1] + 1 == layer.kernel_size[1]
             and layer.padding_mode == "zeros" and not layer._forward_pre_hooks
             and train_ops._lib_k_ok(layer.kernel_size[1], 1))
 

@@ -16,7 +16,7 @@ import sys
 import numpy as np
 import torch
 
-from . import utils
+from . import ops, utils
 from .commons import infer_path
 from .export import load_model
 
@@ -195,11 +195,20 @@ class EmoVITS(object):
                     length_scale=duration_rate)
                 run.static["noise"].copy_(self.noise.float())
             self._graphs[key] = run  # most recently used last
-            start = np.random.randint(2 ** 31 - 1)  # folded into range on the device
-            wav, y_len = run(text_t, emo, sid, noise_start=start, x_length=t_x)
-            n = int(y_len[0])  # (synchronises: the copy below needs it anyway)
+            # infer.py:173's np.random.randint(len - nl), drawn on the device
+            # from raw words of numpy's own generator: the same start as the
+            # reference, and the generator ends where the reference's does
+            pool, state = ops.numpy_draw_pool()
+            wav, y_len = run(text_t, emo, sid, noise_start=pool, x_length=t_x)
+            n, used = (int(v) for v in y_len[:, 0].tolist())  # (synchronises)
             if n <= tyb:
+                if used < 0:
+                    np.random.set_state(state)
+                    raise ValueError(f"utterance of {n} frames does not fit the "
+                                     f"{self.noise.numel()}-sample noise buffer")
+                ops.numpy_draw_commit(state, used)
                 return wav[0, 0, :n * self.hop_size].float().cpu().numpy()
+            np.random.set_state(state)  # re-run at a larger bucket: same draw
             if tyb >= 4096:
                 raise RuntimeError(f"utterance of {n} frames exceeds the 4096-frame noise buffer")
             self._ty_bucket[(xb, duration_rate)] = min(4096, 1 << (n - 1).bit_length())

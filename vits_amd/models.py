@@ -484,8 +484,12 @@ class SynthesizerTrn(nn.Module):
         (ops.length_skip), so the work follows y_len, not t_y.
 
         ``noise``: pre-scaled like infer_p2's (z = m + noise * s): [B, C,
-        t_y], or a flat buffer read from ``noise_start`` (int32 [B]) as
-        EmoVITS slices it.  ``x_lengths`` (int32 [B]): padded text, encoded
+        t_y], or a flat buffer sliced as EmoVITS slices it at
+        np.random.randint(numel - C * y_len), drawn on the device from
+        ``noise_start`` = int32 [B, ops.ED_DRAWS] raw MT19937 words
+        (ops.numpy_draw_pool); the returned y_len is then int32 [2, B]:
+        (y_len, generator words consumed or -1 when the slice does not
+        fit).  ``x_lengths`` (int32 [B]): padded text, encoded
         as TextEncoder.infer of each unpadded utterance (every layer masked,
         engine.TextEncoderPlan pad_exact); None: the exact-length infer_p1
         path (B = 1).  Returns (wav [B, 1, t_y * hop], y_len int32 [B]);
@@ -510,6 +514,8 @@ class SynthesizerTrn(nn.Module):
         with engine.ops.length_skip(64):
             engine.get_plan(self.flow, engine.CouplingFlowPlan).run_(z, gf, lengths=lens[0])
             o = engine.get_plan(self.dec, engine.GeneratorPlan).run(z, gf, lengths=lens[1:])
+        if noise_start is not None:
+            return o.to(m_p.dtype), lens[0::len(lens) - 1]
         return o.to(m_p.dtype), lens[0]
 
     @torch.no_grad()
@@ -520,14 +526,16 @@ class SynthesizerTrn(nn.Module):
         bucket.  noise_len: replay reads a flat noise buffer of that many
         elements at a per-call start offset (EmoVITS); else noise [1, C,
         t_y].  Returns run(x, emo, sid, noise, noise_start=None,
-        x_length=None) -> (wav, y_len) views of static buffers."""
+        x_length=None) -> (wav, y_len) views of static buffers; with
+        noise_len, noise_start is the [ops.ED_DRAWS] raw-word pool of
+        ops.numpy_draw_pool and y_len is [2, 1] (y_len, words consumed)."""
         dev = next(self.parameters()).device
         dt = next(self.parameters()).dtype
         C = self.inter_channels
         static = dict(x=torch.zeros(1, t_x, self.text_channels, device=dev, dtype=dt),
                       emo=torch.zeros(1, 1024, device=dev, dtype=dt),
                       sid=torch.zeros(1, device=dev, dtype=torch.long),
-                      start=torch.zeros(1, device=dev, dtype=torch.int32),
+                      start=torch.zeros(1, engine.ops.ED_DRAWS, device=dev, dtype=torch.int32),
                       xl=torch.full((1,), t_x, device=dev, dtype=torch.int32),
                       noise=torch.zeros(noise_len if noise_len else C * t_y, device=dev))
 
@@ -548,7 +556,7 @@ class SynthesizerTrn(nn.Module):
         with torch.cuda.graph(graph):
             out = body()
 
-        def run(x, emo, sid, noise=None, noise_start=0, x_length=None):
+        def run(x, emo, sid, noise=None, noise_start=None, x_length=None):
             if padded_text:
                 n = x.shape[1] if x_length is None else int(x_length)
                 static["x"].zero_()
@@ -560,7 +568,8 @@ class SynthesizerTrn(nn.Module):
             static["sid"].copy_(sid)
             if noise is not None:
                 static["noise"].copy_(noise.reshape(-1))
-            static["start"].fill_(int(noise_start))
+            if noise_start is not None:
+                static["start"].copy_(torch.as_tensor(noise_start, dtype=torch.int32).view(1, -1))
             graph.replay()
             return out
 

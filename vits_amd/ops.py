@@ -14,6 +14,7 @@ import threading
 from dataclasses import dataclass, field
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -778,6 +779,29 @@ def expand_prior(attn: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor, noise
     return out
 
 
+ED_DRAWS = 32  # VITS_ED_DRAWS (include/vits_amd.h)
+
+
+def numpy_draw_pool(n: int = ED_DRAWS):
+    """The next ``n`` raw 32-bit MT19937 words of numpy's global legacy
+    generator (RandomState.randint over the full uint32 range returns them
+    unmasked, one word each) and the generator state before them.  The
+    device consumes k of them the way ``np.random.randint(high)`` would;
+    ``numpy_draw_commit`` then leaves the generator exactly where that
+    randint call would have left it."""
+    state = np.random.get_state()
+    words = np.random.randint(0, 2 ** 32, size=n, dtype=np.uint32)
+    return words.view(np.int32).copy(), state
+
+
+def numpy_draw_commit(state, used: int) -> None:
+    """Rewind numpy's global generator to ``state`` and advance it by the
+    ``used`` words the device consumed (see numpy_draw_pool)."""
+    np.random.set_state(state)
+    if used > 0:
+        np.random.randint(0, 2 ** 32, size=used, dtype=np.uint32)
+
+
 def expand_durations(logw: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor,
                      noise: torch.Tensor, t_y: int, *, rate: float = 1.0,
                      noise_scale: float = 1.0, x_len: Optional[torch.Tensor] = None,
@@ -790,8 +814,11 @@ def expand_durations(logw: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor,
     m_p + noise * s_p * noise_scale over the static bucket t_y (0 past
     y_len), lens[i] = y_len * stage_mult[i].  ``noise`` is [B, C, t_y], or
     with ``noise_start`` (int32 [B]) a flat buffer read as EmoVITS slices it
-    (element (c, t) at s + c * y_len + t, s = noise_start[b] mod (numel -
-    C * y_len): a raw random draw lands uniformly in the valid range)."""
+    (element (c, t) at s + c * y_len + t): ``noise_start`` is then int32
+    [B, ED_DRAWS] raw MT19937 words (``numpy_draw_pool``) from which the
+    device draws s = np.random.randint(numel - C * y_len) exactly as numpy's
+    legacy RandomState would, and ``lens`` gets one more row: the words
+    consumed per utterance (-1: the slice does not fit, z is zero)."""
     require_device(logw, m_p, s_p, noise)
     B, C_, t_x = m_p.shape
     logw = logw.reshape(B, t_x).float().contiguous()
@@ -801,11 +828,17 @@ def expand_durations(logw: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor,
     if out is None:
         out = torch.empty(B, C_, t_y, device=m_p.device, dtype=torch.float32)
     n_stage = len(stage_mult)
+    rows = n_stage + (0 if noise_start is None else 1)
     if lens is None:
-        lens = torch.empty(n_stage, B, device=m_p.device, dtype=torch.int32)
+        lens = torch.empty(rows, B, device=m_p.device, dtype=torch.int32)
+    if tuple(lens.shape) != (rows, B) or lens.dtype != torch.int32 or not lens.is_contiguous():
+        raise _lib.VitsAmdError(f"expand_durations: lens must be int32 [{rows}, {B}]")
     mult = (C.c_int32 * n_stage)(*[int(v) for v in stage_mult])
     if noise_start is None:
         assert tuple(noise.shape) == (B, C_, t_y), noise.shape
+    elif (tuple(noise_start.shape) != (B, ED_DRAWS) or noise_start.dtype != torch.int32
+          or not noise_start.is_contiguous()):
+        raise _lib.VitsAmdError(f"expand_durations: noise_start must be int32 [{B}, {ED_DRAWS}]")
     check(_lib.load().vits_expand_durations(
         logw.data_ptr(), logw.stride(0), _ptr(x_len), t_x, float(rate), int(half_round),
         m_p.data_ptr(), s_p.data_ptr(), m_p.stride(0), m_p.stride(1), noise.data_ptr(),

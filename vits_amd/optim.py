@@ -58,9 +58,14 @@ class FusedRAdam(torch.optim.Optimizer):
         int (radam.py:69 counts with ``+= 1``), a tensor ``lr`` as a float,
         so a ``D_*.pth`` written here loads into the reference's RAdam."""
         sd = super().state_dict()
+        # torch hands out the live per-parameter state dicts: copy them before
+        # rewriting ``step``, or the live entry (a view of the group's device
+        # counter) would be replaced by a frozen int (ADVICE r03)
+        sd["state"] = {k: dict(v) for k, v in sd["state"].items()}
         for st in sd["state"].values():
             if isinstance(st.get("step"), torch.Tensor):
                 st["step"] = int(round(float(st["step"])))
+        sd["param_groups"] = [dict(g) for g in sd["param_groups"]]
         for g in sd["param_groups"]:
             for k in ("lr", "initial_lr"):
                 if isinstance(g.get(k), torch.Tensor):
