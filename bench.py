@@ -422,12 +422,10 @@ def train_leg(args, device, rank, world, dist, B=None, cpu_base=True):
     batch = [t.to(device) for t in synthetic_batch(hps, B, tx=args.tx, ty=args.ty, seed=rank)]
     graph_err = None
     if use_graph:
-        try:
-            st.capture(batch, warmup=max(1, args.train_warmup))
-        except Exception as e:  # report and time the eager step instead
-            graph_err = f"{type(e).__name__}: {e}"[:300]
-            use_graph = False
-            torch.cuda.synchronize()
+        # a failed capture falls back to eager steps on EVERY rank together
+        # (capture_agreed all-reduces the outcome; warm-up errors propagate)
+        graph_err = st.capture_agreed(batch, warmup=max(1, args.train_warmup))
+        use_graph = graph_err is None
     run = (lambda: st.replay()) if use_graph else (lambda: st.step(batch))
     for _ in range(args.train_warmup):
         run()

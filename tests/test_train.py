@@ -240,6 +240,47 @@ def _ddp_worker(rank, world, port, out_dir, mode="ddp"):
     dist.destroy_process_group()
 
 
+def _capture_fail_worker(rank, world, port, out_dir):
+    """TrainStep.capture_agreed with the graph capture failing on rank 1
+    only: both ranks must report the failure and fall back to eager steps
+    together (the collectives of the eager steps then pair up: no hang)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _patch_cpu()
+    hps = tiny_hps()
+    st = _make(hps, torch.device("cpu"), seed=rank, allreduce=True)
+    batch = _batch(hps, 2, seed=rank)
+
+    def warmup(b, n):  # the eager warm-up steps of _capture_warmup
+        for _ in range(n):
+            st.step(b)
+
+    def graph():
+        if rank == 1:
+            raise RuntimeError("forced capture failure")
+        st.graph = "captured"
+
+    st._capture_warmup, st._capture_graph = warmup, graph
+    err = st.capture_agreed(batch, warmup=1)
+    out = st.step(batch)  # eager on both ranks
+    flat = torch.cat([p.detach().flatten() for p in st.net_g.parameters()])
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), flat.numpy())
+    with open(os.path.join(out_dir, f"err{rank}.txt"), "w") as f:
+        f.write(f"{err}|{st.graph}|{float(out['loss_gen_all'])}")
+    dist.destroy_process_group()
+
+
+def test_capture_failure_on_one_rank_falls_back_on_all_ranks(tmp_path):
+    port = _free_port()
+    mp.spawn(_capture_fail_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    e0 = (tmp_path / "err0.txt").read_text().split("|")
+    e1 = (tmp_path / "err1.txt").read_text().split("|")
+    assert e0[0] == "graph capture failed on another rank" and e0[1] == "None"
+    assert e1[0].startswith("RuntimeError: forced capture failure") and e1[1] == "None"
+    assert np.array_equal(np.load(tmp_path / "rank0.npy"), np.load(tmp_path / "rank1.npy"))
+
+
 @pytest.mark.parametrize("mode", ["ddp", "allreduce"])
 def test_ddp_gloo_world2_replicas_stay_identical(tmp_path, mode):
     """Both multi-process modes (DDP; the graph-capturable flat all-reduce)

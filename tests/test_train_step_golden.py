@@ -126,6 +126,49 @@ def _batch(G, device):
     return out
 
 
+def _run_step(G, cfg, device, fp16):
+    """One step on the golden inputs; returns (step, outputs, G params
+    before, D params before) with the gradients left on the parameters."""
+    st = _make_step(cfg, device, fp16)
+    g0 = {k: p.detach().clone() for k, p in st.net_g.named_parameters()}
+    d0 = {k: p.detach().clone() for k, p in st.net_d.named_parameters()}
+    with _Replay(G):
+        out = st.step(_batch(G, device))
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+        if fp16:
+            assert float(st.scaler.get_scale()) == 1024.0, "the step was skipped (fp16 overflow)"
+    return st, out, g0, d0
+
+
+def _grads(st):
+    """{net.param: fp64 CPU gradient} of both networks after a step."""
+    out = {}
+    for pre, net in (("g.", st.net_g), ("d.", st.net_d)):
+        for k, p in net.named_parameters():
+            if p.grad is not None:
+                out[pre + k] = p.grad.detach().double().cpu().flatten()
+    return out
+
+
+def grad_agreement(ga, gb, gref, rel_floor=1e-3):
+    """Per-parameter agreement of two gradient sets on the same step: for
+    every parameter whose reference gradient norm exceeds ``rel_floor`` of
+    its network's total, the cosine similarity and the norm ratio |a|/|b|.
+    Returns {name: (cos, ratio)}."""
+    tot = {pre: sum(float(v.norm()) ** 2 for k, v in gref.items() if k.startswith(pre)) ** 0.5
+           for pre in ("g.", "d.")}
+    res = {}
+    for k, r in gref.items():
+        if float(r.norm()) <= rel_floor * tot[k[:2]]:
+            continue
+        a, b = ga[k], gb[k]
+        na, nb = float(a.norm()), float(b.norm())
+        cos = float(a @ b) / max(na * nb, 1e-300)
+        res[k] = (cos, na / max(nb, 1e-300))
+    return res
+
+
 def _metrics(G, cfg, device, fp16):
     """Run the step once; return {metric: max relative error} vs the golden.
 
@@ -136,15 +179,7 @@ def _metrics(G, cfg, device, fp16):
     |sum(update) - ref| / sum of |ref update| (AdamW's first step moves
     every weight by +-lr, so this is the fraction of weights whose update
     sign disagrees), since single near-zero gradient elements may flip."""
-    st = _make_step(cfg, device, fp16)
-    g0 = {k: p.detach().clone() for k, p in st.net_g.named_parameters()}
-    d0 = {k: p.detach().clone() for k, p in st.net_d.named_parameters()}
-    with _Replay(G):
-        out = st.step(_batch(G, device))
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-        if fp16:
-            assert float(st.scaler.get_scale()) == 1024.0, "the step was skipped (fp16 overflow)"
+    st, out, g0, d0 = _run_step(G, cfg, device, fp16)
     rep = {}
     for k in ("loss_disc", "loss_gen", "loss_stft", "loss_dur", "loss_kl", "loss_kl_q",
               "loss_gen_all", "sc_loss", "mag_loss"):
@@ -257,3 +292,57 @@ def test_train_step_gpu_fp16_autocast_vs_reference(device, monkeypatch):
     print("torch f16:", {k: f"{v:.2e}" for k, v in ref16.items()})
     for k in hip:
         assert hip[k] <= 2.0 * ref16[k] + 1e-3, (k, hip[k], ref16[k])
+
+
+@pytest.mark.gpu
+def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, monkeypatch):
+    """Per-parameter bar for the fp16 step: the HIP
+    training kernels' gradient of EVERY parameter is compared directly with
+    torch-autocast's gradient of the same parameter on the same step (the
+    reference's own fp16 arithmetic: MIOpen fp16 convs, torch gates), so a
+    bug in one layer's kernels cannot hide inside an aggregate.  Parameters
+    whose fp32 gradient is below 1e-3 of the network's total norm are
+    skipped (fp16 rounding noise dominates them for both paths).
+
+    Bar: cosine >= COS_MIN and norm ratio within NORM_TOL of 1 - except
+    where torch-autocast itself disagrees with the fp32 gradient of the same
+    step (torch fp32 convs) by more than that: there the HIP gradient must
+    be at least as close to fp32 as torch-autocast's is (cos_hip_f32 >=
+    cos_torch_f32 - 0.01)."""
+    from vits_amd import discriminators, train_ops
+
+    G, cfg = _load()
+    st, *_ = _run_step(G, cfg, device, True)
+    g_hip = _grads(st)
+    with monkeypatch.context() as mp:
+        mp.setattr(train_ops, "autocast_wdtype", lambda *a, **k: None)
+        mp.setattr(discriminators, "STFT_D_HIP", False)
+        st, *_ = _run_step(G, cfg, device, True)
+        g_t16 = _grads(st)
+    st, *_ = _run_step(G, cfg, device, False)
+    g_f32 = _grads(st)
+    del st
+    assert set(g_hip) == set(g_t16) == set(g_f32)
+    hip_t16 = grad_agreement(g_hip, g_t16, g_f32)
+    hip_f32 = grad_agreement(g_hip, g_f32, g_f32)
+    t16_f32 = grad_agreement(g_t16, g_f32, g_f32)
+    bad, worst = [], None
+    for k, (cos, ratio) in hip_t16.items():
+        ok = cos >= COS_MIN and abs(ratio - 1.0) <= NORM_TOL
+        if not ok:
+            # torch-autocast itself off the fp32 gradient: HIP must be as close
+            ok = hip_f32[k][0] >= t16_f32[k][0] - 0.01 and t16_f32[k][0] < COS_MIN + 0.005
+        if worst is None or cos < worst[1]:
+            worst = (k, cos, ratio, hip_f32[k][0], t16_f32[k][0])
+        if not ok:
+            bad.append((k, cos, ratio, hip_f32[k][0], t16_f32[k][0]))
+    print(f"{len(hip_t16)} parameters compared; worst cos(HIP16, torch16): "
+          f"{worst[0]} cos={worst[1]:.5f} ratio={worst[2]:.4f} "
+          f"(cos vs fp32: HIP {worst[3]:.5f}, torch16 {worst[4]:.5f})")
+    mn = min(c for c, _ in hip_f32.values())
+    print(f"min cos(HIP16, fp32) = {mn:.5f}; min cos(torch16, fp32) = "
+          f"{min(c for c, _ in t16_f32.values()):.5f}")
+    assert not bad, bad[:10]
+
+
+COS_MIN, NORM_TOL = 0.99, 0.10

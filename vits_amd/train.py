@@ -337,6 +337,47 @@ class TrainStep:
         and the alignment-noise decay runs inside the graph.  Multi-process
         runs capture with allreduce=True (the gradient all-reduce becomes a
         captured RCCL node); DDP's hooks are not capturable."""
+        self._capture_warmup(batch, warmup)
+        return self._capture_graph()
+
+    def capture_agreed(self, batch, warmup: int = 3):
+        """capture() for multi-process runs, with every rank agreeing on the
+        outcome: the eager warm-up steps (they run real all-reduces) let an
+        error propagate - torch.distributed.run then ends every rank - while
+        a failure of the graph capture itself (no real collective runs while
+        capturing) is caught, and one MIN all-reduce of a success flag makes
+        every rank fall back to eager steps together.  A rank that replayed
+        its graph while another stepped eagerly would pair their collectives
+        wrongly and hang.  Returns None on success, else the error text
+        (this rank's, or that another rank failed)."""
+        self._capture_warmup(batch, warmup)
+        err = None
+        try:
+            self._capture_graph()
+        except Exception as e:  # noqa: BLE001 - reported, and agreed below
+            err = f"{type(e).__name__}: {e}"[:300]
+            self.graph = None
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+        if self.allreduce or (dist.is_available() and dist.is_initialized()):
+            ok = torch.tensor([0 if err else 1], device=self.device, dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and err is None:
+                err = "graph capture failed on another rank"
+                self.graph = None
+        if err is not None:
+            self._uncapture()
+        return err
+
+    def _uncapture(self):
+        """Back to eager steps after a failed / abandoned capture: the host
+        slice RNG and host-side alignment-noise decay of step()."""
+        g_mod = self.net_g
+        g_mod.__dict__.pop("_device_slice_rng", None)
+        g_mod.__dict__.pop("_align_noise_t", None)
+        self.graph = None
+
+    def _capture_warmup(self, batch, warmup):
         assert self.capturable, "TrainStep(capturable=True) is required"
         assert not isinstance(self.net_g, DDP), \
             "DDP's hooks are not capturable: use TrainStep(allreduce=True) for multi-process capture"
@@ -355,6 +396,8 @@ class TrainStep:
                 self.step(self.static)
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+
+    def _capture_graph(self):
         self._release_autograd_refs()
         self.graph = torch.cuda.CUDAGraph()
         self.optim_g.zero_grad(set_to_none=True)
