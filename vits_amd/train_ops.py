@@ -68,6 +68,7 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
 # kernel's two-stage global->LDS pipeline; at kc = 16 a 1x1 conv has one
 # MFMA k-step per chunk and waits on every chunk's loads.
 TRAIN_KCK = int(os.environ.get("VITS_TRAIN_KCK", "64"))
+_GA_ALL = os.environ.get("VITS_GA16") == "2"  # weights from global memory: no W LDS budget
 _TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32}
 _TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256}
 
@@ -81,7 +82,7 @@ def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
     xrs = bn + (k - 1) * dil + 8
     xbudget = (6144 if bn <= 128 else 10240) if io16 else (3072 if bn <= 128 else 5120)
     for kc in (64, 48, 32):
-        if (kc * k <= TRAIN_KCK and cin_pad % kc == 0 and kc * k * bm // 2 <= 6144
+        if (kc * k <= TRAIN_KCK and cin_pad % kc == 0 and (_GA_ALL or kc * k * bm // 2 <= 6144)
                 and kc * xrs <= xbudget):
             return kc
     return 16
@@ -652,6 +653,54 @@ def _poly_index(K: int, u: int, p: int, device):
     return _POLY_INDEX[key]
 
 
+_POLY_PERM = {}
+
+
+def _poly_perm(C: int, O: int, K: int, u: int, p: int, device):
+    """Flat gather maps of the polyphase weight: fwd[e] = the index into the
+    [C, O, K] weight of element e of the [O*u, C, P+1] phase image (K*C*O
+    of its entries; -1 for the structural zeros), and bwd = its inverse
+    (every tap of W lands in exactly one phase slot, see _poly_index), so
+    the weight gradient is a plain gather too - no index_put accumulation
+    (torch's advanced-index backward: a sort + 0.44 ms for ups.0)."""
+    key = (C, O, K, u, p, str(device))
+    if key not in _POLY_PERM:
+        idx, ok = _poly_index(K, u, p, "cpu")          # [u, P+1]
+        P1 = idx.shape[1]
+        o = torch.arange(O).view(O, 1, 1, 1)
+        r = torch.arange(u).view(1, u, 1, 1)
+        c = torch.arange(C).view(1, 1, C, 1)
+        i = torch.arange(P1).view(1, 1, 1, P1)
+        src = (c * O + o) * K + idx[r, i]              # [O, u, C, P+1]
+        fwd = torch.where(ok[r, i], src, torch.full_like(src, -1)).reshape(-1)
+        bwd = torch.empty(C * O * K, dtype=torch.long)
+        valid = fwd >= 0
+        bwd[fwd[valid]] = torch.nonzero(valid).squeeze(1)
+        assert int(valid.sum()) == C * O * K  # a bijection onto the taps
+        _POLY_PERM[key] = (fwd.clamp(min=0).to(device), valid.to(device), bwd.to(device), P1)
+    return _POLY_PERM[key]
+
+
+class PolyphaseWeight(torch.autograd.Function):
+    """W [C, O, K] of ConvTranspose1d(K, stride u, padding p) -> the phase-
+    stacked stride-1 weight [O*u, C, P+1] of conv_transpose1d's lowering;
+    forward and backward are one gather each."""
+
+    @staticmethod
+    def forward(ctx, w, u: int, p: int):
+        C, O, K = w.shape
+        fwd, valid, bwd, P1 = _poly_perm(C, O, K, u, p, w.device)
+        ctx.conf = (C, O, K, u, p)
+        wp = w.reshape(-1).index_select(0, fwd) * valid.to(w.dtype)
+        return wp.view(O * u, C, P1)
+
+    @staticmethod
+    def backward(ctx, g):
+        C, O, K, u, p = ctx.conf
+        _, _, bwd, _ = _poly_perm(C, O, K, u, p, g.device)
+        return g.contiguous().view(-1).index_select(0, bwd).view(C, O, K), None, None
+
+
 def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) -> torch.Tensor:
     """``module(leaky_relu(x, in_slope))`` for an nn.ConvTranspose1d
     (optionally legacy-weight-normed, output_padding 0, groups 1, dilation 1).
@@ -681,10 +730,7 @@ def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) 
         return module(x)
     w = weight_norm_effective(module)                  # [C, O, K]
     C, O = w.shape[0], w.shape[1]
-    idx, valid = _poly_index(K, u, p, w.device)        # [u, P+1]
-    wt = w.permute(1, 0, 2)                            # [O, C, K]
-    wp = wt[:, :, idx] * valid.to(w.dtype)             # [O, C, u, P+1]
-    wp = wp.permute(0, 2, 1, 3).reshape(O * u, C, P + 1)
+    wp = PolyphaseWeight.apply(w, u, p)                # [O*u, C, P+1]
     bias = None if module.bias is None else module.bias.repeat_interleave(u)
     B, _, T = x.shape
     y = conv1d_hip(x, wp, bias, 1, P - 1 - c0, in_slope, wdt)  # [B, O*u, >= T]
