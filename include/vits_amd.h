@@ -376,6 +376,19 @@ int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, 
 int vits_conv1d_pack16_pair(const float* w, int cout, int cin, int k, void* out, int m_pad,
                             int cin_pad, void* out_t, int m_pad_t, int cin_pad_t, int wdtype,
                             void* stream);
+/* Both images of many layers in few launches (48 layers per launch): the  */
+/* training step packs every HIP conv of a network once per forward, right  */
+/* after the weight / spectral norm launch that produced the weights,       */
+/* instead of one vits_conv1d_pack16_pair launch per conv call.             */
+typedef struct vits_pack16_layer {
+  const float* w;   /* fp32 [cout][cin][k] */
+  int32_t cout, cin, k;
+  void* img;        /* [cin_pad/16][k][2][m_pad][8], rows cout */
+  int32_t m_pad, cin_pad;
+  void* img_t;      /* [cin_pad_t/16][k][2][m_pad_t][8], rows cin, taps reversed */
+  int32_t m_pad_t, cin_pad_t;
+} vits_pack16_layer;
+int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, int wdtype, void* stream);
 
 typedef struct vits_conv1d_wgrad_desc {
   const float* dy;        /* output gradient [B][cout][n_out], t contiguous  */

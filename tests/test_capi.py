@@ -40,19 +40,20 @@ def test_struct_layout_matches_header():
     import subprocess
     import tempfile
 
-    from vits_amd._lib import (WNORM_MAX, SNORM_MAX, ConvDesc, ConvOut, ResblockPairDesc,
-                               SnormLayer, StftJob, WnormLayer)
+    from vits_amd._lib import (WNORM_MAX, SNORM_MAX, ConvDesc, ConvOut, Pack16Layer,
+                               ResblockPairDesc, SnormLayer, StftJob, WnormLayer)
 
     probe = r'''
 #include <stdio.h>
 #include <stddef.h>
 #include "vits_amd.h"
-int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d\n", sizeof(vits_conv1d_desc),
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu %zu %zu\n", sizeof(vits_conv1d_desc),
  sizeof(vits_conv_out), offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths),
  offsetof(vits_conv1d_desc, wdtype), sizeof(vits_stft_job), offsetof(vits_stft_job, eps),
  sizeof(vits_resblock_pair_desc), offsetof(vits_resblock_pair_desc, w2),
  offsetof(vits_resblock_pair_desc, post_div), sizeof(vits_wnorm_layer),
- sizeof(vits_snorm_layer), offsetof(vits_snorm_layer, eps), VITS_WNORM_MAX, VITS_SNORM_MAX);
+ sizeof(vits_snorm_layer), offsetof(vits_snorm_layer, eps), VITS_WNORM_MAX, VITS_SNORM_MAX,
+ sizeof(vits_pack16_layer), offsetof(vits_pack16_layer, img_t), offsetof(vits_pack16_layer, cin_pad_t));
  return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -76,3 +77,6 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d\n",
     assert int(out[11]) == ctypes.sizeof(SnormLayer)
     assert int(out[12]) == SnormLayer.eps.offset
     assert int(out[13]) == WNORM_MAX and int(out[14]) == SNORM_MAX
+    assert int(out[15]) == ctypes.sizeof(Pack16Layer)
+    assert int(out[16]) == Pack16Layer.img_t.offset
+    assert int(out[17]) == Pack16Layer.cin_pad_t.offset

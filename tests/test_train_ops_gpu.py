@@ -424,3 +424,51 @@ def test_layer_norm_hip_fwd_bwd(device, monkeypatch, B, C, T):
         got = got.detach().double().cpu()
         err = (got - ref.detach()).abs().max().item() / ref.detach().abs().max().item()
         assert err < 2e-5, (what, err)
+
+
+def test_prepacked_network_bitwise_equals_per_call_pack(device):
+    """train_ops.prepacked: the 16-bit images of every HIP conv of a network
+    packed in one vits_conv1d_pack16_pairs launch (48 layers per launch) give
+    bit-identical outputs and gradients to the per-call
+    vits_conv1d_pack16_pair path, for a mix of shapes (k 1..11, dilations,
+    ragged channel counts, more layers than one launch holds)."""
+    torch.manual_seed(3)
+    specs = [(20, 36, 5, 1), (36, 64, 3, 3), (64, 17, 11, 1), (17, 40, 1, 1), (40, 40, 7, 2)]
+    layers = torch.nn.ModuleList()
+    for i in range(60):  # > 48: two launches
+        cin, cout, k, dil = specs[i % len(specs)]
+        if i > 0:
+            cin = layers[-1].out_channels
+        layers.append(torch.nn.Conv1d(cin, cout, k, dilation=dil, padding=dil * (k - 1) // 2))
+    net = layers.to(device)
+    x = torch.randn(2, 20, 136, device=device)
+
+    def run(pre):
+        for p in net.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.float16):
+            ctx = train_ops.prepacked(net) if pre else torch.autocast("cuda", enabled=True,
+                                                                      dtype=torch.float16)
+            with ctx:
+                h = xi
+                for i, m in enumerate(net):
+                    h = train_ops.conv1d(m, h, in_slope=0.1 if i % 2 else 1.0)
+        h.float().square().mean().backward()
+        return h.detach().clone(), xi.grad.clone(), [p.grad.clone() for p in net.parameters()]
+
+    a = run(False)
+    orig = train_ops._pack16_pair
+
+    def no_pack(*args, **kw):
+        raise AssertionError("per-call pack inside a prepacked scope")
+
+    train_ops._pack16_pair = no_pack
+    try:
+        b = run(True)
+    finally:
+        train_ops._pack16_pair = orig
+    assert not train_ops._PREPACK  # scope cleared
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for ga, gb in zip(a[2], b[2]):
+        assert torch.equal(ga, gb)

@@ -179,6 +179,21 @@ WNORM_MAX = 56
 SNORM_MAX = 48
 
 
+class Pack16Layer(C.Structure):
+    _fields_ = [
+        ("w", C.c_void_p),
+        ("cout", C.c_int32),
+        ("cin", C.c_int32),
+        ("k", C.c_int32),
+        ("img", C.c_void_p),
+        ("m_pad", C.c_int32),
+        ("cin_pad", C.c_int32),
+        ("img_t", C.c_void_p),
+        ("m_pad_t", C.c_int32),
+        ("cin_pad_t", C.c_int32),
+    ]
+
+
 class WnormLayer(C.Structure):
     _fields_ = [
         ("v", C.c_void_p),
@@ -294,6 +309,8 @@ _SIGS = {
         [C.c_void_p] + [C.c_int] * 3 + [C.c_void_p] + [C.c_int] * 2 + [C.c_void_p]
         + [C.c_int] * 3 + [C.c_void_p],
     ),
+    "vits_conv1d_pack16_pairs": (C.c_int, [C.POINTER(Pack16Layer), C.c_int, C.c_int,
+                                           C.c_void_p]),
     "vits_conv1d_wgrad": (C.c_int, [C.POINTER(ConvWgradDesc), C.c_int, C.c_void_p]),
     "vits_conv1d_wgrad_workspace": (C.c_int64, [C.POINTER(ConvWgradDesc), C.c_int]),
     "vits_conv1d_wgrad_split": (C.c_int, [C.POINTER(ConvWgradDesc), C.c_int, C.c_void_p,

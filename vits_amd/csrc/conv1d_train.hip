@@ -601,6 +601,34 @@ __global__ void pack16_pair_kernel(const float* __restrict__ w, int cout, int ci
   }
 }
 
+// both images of up to PACK_LIST layers per launch (vits_conv1d_pack16_pairs):
+// the flat index runs over the layers' concatenated images, start[] holds
+// each layer's first element
+constexpr int PACK_LIST = 48;
+struct PackList {
+  vits_pack16_layer l[PACK_LIST];
+  int64_t start[PACK_LIST + 1];
+  int n;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack16_pairs_kernel(const PackList L) {
+  const int64_t end = L.start[L.n];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < end;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int q = 0;
+    while (q + 1 < L.n && L.start[q + 1] <= i) ++q;  // (layers in order; <= 48)
+    const vits_pack16_layer& e = L.l[q];
+    const int64_t total = (int64_t)e.cin_pad * e.k * e.m_pad;
+    const int64_t r = i - L.start[q];
+    if (r < total)
+      pack16_elem<T>(e.w, e.cout, e.cin, e.k, 0, reinterpret_cast<T*>(e.img), e.m_pad, r);
+    else
+      pack16_elem<T>(e.w, e.cout, e.cin, e.k, 1, reinterpret_cast<T*>(e.img_t), e.m_pad_t,
+                     r - total);
+  }
+}
+
 template <typename T>
 __global__ void pack16_kernel(const float* __restrict__ w, int cout, int cin, int k, int transpose,
                               T* __restrict__ out, int m_pad, int cin_pad,
@@ -744,4 +772,36 @@ extern "C" int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int 
   else
     return VITS_E_ARG;
   return vits_launch_status();
+}
+
+extern "C" int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, int wdtype,
+                                        void* stream) {
+  VITS_CHECK_ARG(n >= 0 && (n == 0 || layers));
+  VITS_CHECK_ARG(wdtype == VITS_WDT_F16 || wdtype == VITS_WDT_BF16);
+  hipStream_t s = as_stream(stream);
+  for (int b0 = 0; b0 < n; b0 += PACK_LIST) {
+    PackList L;
+    L.n = n - b0 < PACK_LIST ? n - b0 : PACK_LIST;
+    L.start[0] = 0;
+    for (int q = 0; q < L.n; ++q) {
+      const vits_pack16_layer& e = layers[b0 + q];
+      VITS_CHECK_ARG(e.w && e.img && e.img_t && e.cout > 0 && e.cin > 0 && e.k > 0);
+      VITS_CHECK_SHAPE(e.m_pad % 128 == 0 && e.m_pad >= e.cout && e.cin_pad % 16 == 0 &&
+                       e.cin_pad >= e.cin);
+      VITS_CHECK_SHAPE(e.m_pad_t % 128 == 0 && e.m_pad_t >= e.cin && e.cin_pad_t % 16 == 0 &&
+                       e.cin_pad_t >= e.cout);
+      L.l[q] = e;
+      L.start[q + 1] = L.start[q] + (int64_t)e.cin_pad * e.k * e.m_pad +
+                       (int64_t)e.cin_pad_t * e.k * e.m_pad_t;
+    }
+    const int64_t nblk = (L.start[L.n] + 255) / 256;
+    const int blocks = (int)(nblk < 8192 ? nblk : 8192);
+    if (wdtype == VITS_WDT_F16)
+      hipLaunchKernelGGL(pack16_pairs_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, L);
+    else
+      hipLaunchKernelGGL(pack16_pairs_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, L);
+    const int rc = vits_launch_status();
+    if (rc) return rc;
+  }
+  return VITS_OK;
 }

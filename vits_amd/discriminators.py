@@ -309,7 +309,10 @@ class MultiWaveSTFTDiscriminator(nn.Module):
         """x [B, 1, t] waveform, m list of STFT magnitudes [B, F, T] (the
         MR-STFT loss's outputs, train_stft.py:198-199)."""
         self._sn.apply(self.training)
-        return self.mwd(x) + self.mfd(m)
+        # every HIP conv's 16-bit images from the W / sigma just computed, in
+        # one launch (instead of one pack per conv call)
+        with train_ops.prepacked(self):
+            return self.mwd(x) + self.mfd(m)
 
 
 # ---------------------------------------------------------------------------

@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 from torch.nn.parallel import DistributedDataParallel as DDP
 
-from . import commons, utils
+from . import commons, train_ops, utils
 from .discriminators import MultiWaveSTFTDiscriminator
 from .losses import discriminator_loss, feature_loss, generator_loss, kl_loss
 from .mel_processing import mel_spectrogram_torch, spec_to_mel_torch
@@ -153,7 +153,7 @@ class TrainStep:
         x, x_lengths, spec, spec_lengths, y, y_lengths, emo, speakers = (
             t.to(self.device, non_blocking=True) for t in batch)
         with self.autocast():
-            with rf("step:G.forward"), self._g_weights():
+            with rf("step:G.forward"), self._g_weights(), train_ops.prepacked(self.net_g):
                 (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
                  (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
                     x, x_lengths, spec, spec_lengths, emo, speakers)
@@ -239,7 +239,7 @@ class TrainStep:
             t.to(self.device, non_blocking=True) for t in batch)
         seg = hps.train.segment_size // hps.data.hop_length
         with self.autocast():
-            with rf("step:G.forward"), self._g_weights():
+            with rf("step:G.forward"), self._g_weights(), train_ops.prepacked(self.net_g):
                 (y_hat, l_length, attn, ids_slice, x_mask, z_mask,
                  (z, z_p, m_p, logs_p, m_q, logs_q), z_q, (x_hidden, logw, logw_)) = self.net_g(
                     x, x_lengths, spec, spec_lengths, emo, speakers)

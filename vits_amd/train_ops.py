@@ -32,6 +32,7 @@ torch conv, i.e. the reference's own fp32 arithmetic.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -127,6 +128,77 @@ def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
     bwd = PackedConv(img_t, None, cout, cin, k, dil, (k - 1) * dil - pad_left, EPI_STORE, tb,
                      _train_kc(cin_pad_t, k, dil, tb, io16), out_channels=cin, wdtype=wdtype)
     return fwd, bwd
+
+
+def _layers16(pre, shape, dil: int, pad_left: int, wdtype: int, bias, n_out: int, n_in: int):
+    """(forward PackedConv, input-gradient PackedConv) around prepacked
+    images (img, img_t) of a [cout, cin, k] weight (the 16-bit activation
+    path, io16)."""
+    img, img_t = pre
+    cout, cin, k = shape
+    tf, tb = _pick_tile_train(cout, k, n_out), _pick_tile_train(cin, k, n_in)
+    fwd = PackedConv(img, bias, cin, cout, k, dil, pad_left, EPI_STORE, tf,
+                     _train_kc(img.shape[0] * 16, k, dil, tf, True), out_channels=cout,
+                     wdtype=wdtype)
+    bwd = PackedConv(img_t, None, cout, cin, k, dil, (k - 1) * dil - pad_left, EPI_STORE, tb,
+                     _train_kc(img_t.shape[0] * 16, k, dil, tb, True), out_channels=cin,
+                     wdtype=wdtype)
+    return fwd, bwd
+
+
+# module -> (weight tensor, (img, img_t), wdtype): the images of every HIP
+# conv of a network packed in one launch per 48 layers (prepacked) and used
+# by conv1d() while the same weight tensor is served
+_PREPACK: dict = {}
+
+
+@contextlib.contextmanager
+def prepacked(net: nn.Module):
+    """Inside a 16-bit autocast region on the GPU: pack the 16-bit forward
+    and input-gradient images of every Conv1d of ``net`` that ``conv1d``
+    runs on the HIP kernels, from the weights it will be served (the active
+    weight-norm cache's or the module's own), with ONE
+    ``vits_conv1d_pack16_pairs`` launch per 48 layers instead of one
+    ``vits_conv1d_pack16_pair`` launch per conv call.  The images are valid
+    for this scope only (the weights change at the next optimizer step)."""
+    wdt = autocast_wdtype("cuda")
+    mods = []
+    if wdt is not None and _io16(wdt):
+        mods = [m for m in net.modules() if supported(m)
+                and any(p.is_cuda for p in m.parameters(recurse=False))]
+    if not mods:
+        yield
+        return
+    items, arr = [], (_lib.Pack16Layer * len(mods))()
+    dt = _TORCH_16[wdt]
+    for i, m in enumerate(mods):
+        w = weight_norm_effective(m)
+        w32 = w.detach()
+        if w32.dtype != torch.float32 or not w32.is_contiguous():
+            w32 = w32.float().contiguous()
+        cout, cin, k = w32.shape
+        m_pad, cin_pad = (cout + 127) // 128 * 128, (cin + 15) // 16 * 16
+        m_pad_t, cin_pad_t = (cin + 127) // 128 * 128, (cout + 15) // 16 * 16
+        img = torch.empty(cin_pad // 16, k, 2, m_pad, 8, dtype=dt, device=w32.device)
+        img_t = torch.empty(cin_pad_t // 16, k, 2, m_pad_t, 8, dtype=dt, device=w32.device)
+        e = arr[i]
+        e.w, e.cout, e.cin, e.k = w32.data_ptr(), cout, cin, k
+        e.img, e.m_pad, e.cin_pad = img.data_ptr(), m_pad, cin_pad
+        e.img_t, e.m_pad_t, e.cin_pad_t = img_t.data_ptr(), m_pad_t, cin_pad_t
+        items.append((m, (w, (img, img_t), wdt), w32))
+    check(_lib.load().vits_conv1d_pack16_pairs(arr, len(mods), wdt, _stream_ptr(items[0][2].device)),
+          "vits_conv1d_pack16_pairs")
+    prev = {m: _PREPACK.get(m) for m, _, _ in items}
+    for m, ent, _ in items:
+        _PREPACK[m] = ent
+    try:
+        yield
+    finally:
+        for m, old in prev.items():
+            if old is None:
+                _PREPACK.pop(m, None)
+            else:
+                _PREPACK[m] = old
 
 
 def _run(x: torch.Tensor, layer: PackedConv, n_out: int, in_slope: float = 1.0,
@@ -324,16 +396,22 @@ class Conv1dHip16(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, dilation: int, padding: int, in_slope: float, wdtype: int,
-                res=None):
+                res=None, pre=None):
         """res (optional, fp16 [B, Cout, n_out]): y = res + conv, the
-        residual add of ResBlock2 (modules.py:258-259) in the epilogue."""
+        residual add of ResBlock2 (modules.py:258-259) in the epilogue.
+        pre (optional): (img, img_t) of ``weight`` already packed by
+        ``prepacked`` (one launch for the whole network)."""
         if x.stride(2) != 1:
             x = x.contiguous()
         w32 = weight.detach().float().contiguous()
         k = w32.shape[2]
         n_out = x.shape[2] + 2 * padding - (k - 1) * dilation
         b32 = None if bias is None else bias.detach().float().contiguous()
-        if ctx.needs_input_grad[0]:
+        if pre is not None:
+            layer, layer_t = _layers16(pre, w32.shape, dilation, padding, wdtype, b32, n_out,
+                                       x.shape[2])
+            ctx.layer_t = layer_t
+        elif ctx.needs_input_grad[0]:
             layer, layer_t = _pack16_pair(w32, dilation, padding, wdtype, b32, n_out, x.shape[2],
                                           io16=True)
             ctx.layer_t = layer_t
@@ -370,10 +448,11 @@ class Conv1dHip16(torch.autograd.Function):
         if want_w:
             dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype,
                            split=True)
-        if len(ctx.needs_input_grad) == 7:  # called without the residual argument
-            return dx, dw, db, None, None, None, None
-        dres = dy if ctx.needs_input_grad[7] else None
-        return dx, dw, db, None, None, None, None, dres
+        grads = [dx, dw, db, None, None, None, None]
+        if len(ctx.needs_input_grad) > 7:  # the residual argument
+            grads.append(dy if ctx.needs_input_grad[7] else None)
+        grads += [None] * (len(ctx.needs_input_grad) - len(grads))
+        return tuple(grads)
 
 
 # modules.LayerNorm on the HIP kernels on the GPU (VITS_LN_HIP=1).  Off by
@@ -513,19 +592,20 @@ def _io16(wdt) -> bool:
 
 
 def conv1d_hip(x: torch.Tensor, w: torch.Tensor, bias, dilation: int, padding: int,
-               in_slope: float, wdt: int, residual: torch.Tensor | None = None) -> torch.Tensor:
+               in_slope: float, wdt: int, residual: torch.Tensor | None = None,
+               pre=None) -> torch.Tensor:
     """The HIP training conv of operand type ``wdt`` (+ ``residual``): 16-bit
     activations (Conv1dHip16; x cast to fp16 first, as autocast casts a
     conv's input; the residual added in the epilogue) or fp32 activations
-    (Conv1dHip)."""
+    (Conv1dHip).  ``pre``: the weight's prepacked images (``prepacked``)."""
     if _io16(wdt):
         t16 = _TORCH_16[wdt]
         x16 = x if x.dtype == t16 else x.to(t16)
         if residual is not None and residual.dtype != t16:
             # an fp32 residual stream keeps the reference's fp32 add
             return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt,
-                                     None) + residual
-        return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt, residual)
+                                     None, pre) + residual
+        return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt, residual, pre)
     y = Conv1dHip.apply(x, w, bias, dilation, padding, in_slope, wdt)
     return y if residual is None else y + residual
 
@@ -611,8 +691,10 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0,
         t16 = _TORCH_16[wdt]
         y = torch.matmul(w[:, :, 0].to(t16), x.to(t16))
         return y if module.bias is None else y + module.bias.to(t16)[:, None]
+    ent = _PREPACK.get(module)
+    pre = ent[1] if (ent is not None and ent[0] is w and ent[2] == wdt) else None
     return conv1d_hip(x, w, module.bias, module.dilation[0], module.padding[0], in_slope, wdt,
-                      residual)
+                      residual, pre)
 
 
 # 1x1 training convs with T <= this run as hipBLASLt GEMMs (0: always the HIP conv)
