@@ -35,6 +35,7 @@
  *                            (stft_loss.py:47-95) in one launch
  *   vits_layer_norm_channels modules.LayerNorm (modules.py:41-44)
  *   vits_attention_forward   MultiHeadAttention.attention core
+ *   vits_attention_train_*   the same under autograd (dropout; backward)
  *                            (attentions.py:85-100)
  */
 #ifndef VITS_AMD_H
@@ -351,6 +352,27 @@ int vits_attention_forward(const float* q, const float* k, const float* v, float
                            int batch, int heads, int head_dim, int t_len,
                            int64_t qkv_bstride, int64_t out_bstride, const int32_t* lengths,
                            void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* Training attention (MultiHeadAttention.attention, attentions.py:85-100, */
+/* under autograd with p_dropout): q/k/v/out contiguous [B][H*D][T] of     */
+/* dtype VITS_WDT_F16 (the fp16 projection convs' outputs) or _F32, fp32   */
+/* MFMA arithmetic; mask from lengths (scores.masked_fill(-1e4) of the      */
+/* x_mask outer product); keep [B][H][T][T] uint8 (NULL: no dropout)        */
+/* scales the probabilities by keep * keep_scale as nn.Dropout does.       */
+/* The forward writes lse [B][H][T] (fp32 log-sum-exp per query) for the    */
+/* backward, which recomputes P and writes dq, dk, dv (same layout/dtype);  */
+/* delta [B][H][T] fp32 is its scratch.  head_dim in {32, 64, 96, 128}.    */
+/* ---------------------------------------------------------------------- */
+int vits_attention_train_forward(const void* q, const void* k, const void* v,
+                                 const uint8_t* keep, float keep_scale, void* out, float* lse,
+                                 int batch, int heads, int head_dim, int t_len,
+                                 const int32_t* lengths, int dtype, void* stream);
+int vits_attention_train_backward(const void* q, const void* k, const void* v, const void* out,
+                                  const void* dout, const uint8_t* keep, float keep_scale,
+                                  const float* lse, float* delta, void* dq, void* dk, void* dv,
+                                  int batch, int heads, int head_dim, int t_len,
+                                  const int32_t* lengths, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------- */
 /* Training-step convs (backward of every stride-1 nn.Conv1d the          */

@@ -5,6 +5,8 @@ autocast convs round them, train_stft.py:165).  With identical operands the
 only difference is fp32 summation order, so the tolerance is 2e-4 of each
 tensor's max magnitude (the bias-free check below uses the unrounded dY for
 dbias, which the kernel sums in fp32 before rounding)."""
+import math
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -472,3 +474,70 @@ def test_prepacked_network_bitwise_equals_per_call_pack(device):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     for ga, gb in zip(a[2], b[2]):
         assert torch.equal(ga, gb)
+
+
+def _attn_ref(q, k, v, lengths, heads, keep, p):
+    """attentions.py:85-100 in fp64: masked_fill(-1e4) of the x_mask outer
+    product, softmax, nn.Dropout with the given keep mask, PV."""
+    B, C, T = q.shape
+    D = C // heads
+    qh = q.view(B, heads, D, T).transpose(2, 3)
+    kh = k.view(B, heads, D, T).transpose(2, 3)
+    vh = v.view(B, heads, D, T).transpose(2, 3)
+    xm = (torch.arange(T, device=q.device)[None] < lengths[:, None]).to(q.dtype)
+    mask = (xm[:, None, :, None] * xm[:, None, None, :])
+    s = torch.matmul(qh / math.sqrt(D), kh.transpose(-2, -1)).masked_fill(mask == 0, -1e4)
+    pa = torch.softmax(s, dim=-1)
+    if keep is not None:
+        pa = pa * keep.to(q.dtype) / (1 - p)
+    return torch.matmul(pa, vh).transpose(2, 3).reshape(B, C, T)
+
+
+@pytest.mark.parametrize("dtype,T,D,p", [(torch.float32, 77, 128, 0.1), (torch.float32, 100, 64, 0.0),
+                                         (torch.float16, 100, 128, 0.1), (torch.float32, 33, 32, 0.3)])
+def test_attention_train_fwd_bwd_vs_torch(device, dtype, T, D, p):
+    """train_ops.AttentionHip (vits_attention_train_forward / _backward)
+    against attentions.py:85-100 in fp64 on the same (rounded) inputs and the
+    same dropout keep mask: output and dq / dk / dv within 1e-4 of the
+    tensor's max for fp32 inputs (fp16 inputs: 2e-3, the fp16 rounding of
+    the stored results)."""
+    torch.manual_seed(0)
+    B, H = 3, 2
+    C = H * D
+    q, k, v = (torch.randn(B, C, T, device=device).to(dtype) for _ in range(3))
+    lengths = torch.tensor([T, T - 9, 5], device=device, dtype=torch.int32)
+    keep = (torch.rand(B, H, T, T, device=device) >= p).to(torch.uint8) if p > 0 else None
+    dout = torch.randn(B, C, T, device=device).to(dtype)
+    qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+    out = train_ops.AttentionHip.apply(qa, ka, va, lengths, H, keep, p)
+    out.backward(dout)
+    q64, k64, v64 = (t.double().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(q64, k64, v64, lengths.long(), H, keep, p)
+    ref.backward(dout.double())
+    tol = 1e-4 if dtype == torch.float32 else 2e-3
+    for got, want, what in ((out, ref, "out"), (qa.grad, q64.grad, "dq"), (ka.grad, k64.grad, "dk"),
+                            (va.grad, v64.grad, "dv")):
+        assert got.dtype == dtype
+        err = (got.double() - want).abs().max().item() / want.abs().max().item()
+        assert err <= tol, (what, err)
+
+
+def test_attention_train_dropout_statistics(device):
+    """train_ops.attention under autocast: the keep mask is drawn with keep
+    probability 1 - p (nn.Dropout's law), and the eval path (training=False)
+    equals the dropout-free kernel."""
+    torch.manual_seed(1)
+    B, H, D, T = 4, 2, 64, 96
+    q, k, v = (torch.randn(B, H * D, T, device=device).half() for _ in range(3))
+    lengths = torch.full((B,), T, device=device, dtype=torch.int32)
+    with torch.autocast("cuda", dtype=torch.float16):
+        y0 = train_ops.attention(q, k, v, H, lengths, 0.1, training=False)
+        y1 = train_ops.AttentionHip.apply(q, k, v, lengths, H, None, 0.0)
+    assert torch.equal(y0, y1)
+    with torch.autocast("cuda", dtype=torch.float16):
+        torch.manual_seed(5)
+        ya = train_ops.attention(q, k, v, H, lengths, 0.1, training=True)
+        torch.manual_seed(5)
+        yb = train_ops.attention(q, k, v, H, lengths, 0.1, training=True)
+        yc = train_ops.attention(q, k, v, H, lengths, 0.1, training=True)
+    assert torch.equal(ya, yb) and not torch.equal(ya, yc) and not torch.equal(ya, y0)

@@ -299,6 +299,16 @@ _SIGS = {
         C.c_int,
         [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p],
     ),
+    "vits_attention_train_forward": (
+        C.c_int,
+        [C.c_void_p] * 4 + [C.c_float] + [C.c_void_p] * 2 + [C.c_int] * 4
+        + [C.c_void_p, C.c_int, C.c_void_p],
+    ),
+    "vits_attention_train_backward": (
+        C.c_int,
+        [C.c_void_p] * 6 + [C.c_float] + [C.c_void_p] * 5 + [C.c_int] * 4
+        + [C.c_void_p, C.c_int, C.c_void_p],
+    ),
     "vits_conv1d_pack16": (
         C.c_int,
         [C.c_void_p] + [C.c_int] * 4 + [C.c_void_p] + [C.c_int] * 3

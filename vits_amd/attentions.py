@@ -37,11 +37,18 @@ class MultiHeadAttention(nn.Module):
         nn.init.xavier_uniform_(self.conv_k.weight)
         nn.init.xavier_uniform_(self.conv_v.weight)
 
-    def forward(self, x, c, attn_mask=None):
+    def forward(self, x, c, attn_mask=None, lengths=None):
+        """lengths (int [B], optional): the key / query lengths attn_mask was
+        built from (Encoder: x_mask outer product); with it, under autocast
+        on the GPU, the attention core runs on the HIP training kernels
+        (train_ops.AttentionHip: MFMA forward + backward, dropout fused)."""
         # 1x1 projections on the HIP training conv under autocast (torch otherwise)
         conv = train_ops.conv1d
         q, k, v = conv(self.conv_q, x), conv(self.conv_k, c), conv(self.conv_v, c)
-        return conv(self.conv_o, self.attention(q, k, v, mask=attn_mask)[0])
+        y = train_ops.attention(q, k, v, self.n_heads, lengths, self.p_dropout, self.training)
+        if y is None:
+            y = self.attention(q, k, v, mask=attn_mask)[0]
+        return conv(self.conv_o, y)
 
     def attention(self, query, key, value, mask=None):
         b, d, t_s = key.size()
@@ -122,9 +129,12 @@ class Encoder(nn.Module):
 
     def forward(self, x, x_mask, g):
         attn_mask = x_mask.unsqueeze(2) * x_mask.unsqueeze(-1)
+        # (x_mask is a length mask, commons.sequence_mask: its row sums are
+        # the lengths the HIP attention masks with)
+        lengths = x_mask[:, 0].sum(-1).to(torch.int32) if x_mask.is_cuda else None
         x = x * x_mask
         for i in range(self.n_layers):
-            y = self.drop(self.attn_layers[i](x, x, attn_mask))
+            y = self.drop(self.attn_layers[i](x, x, attn_mask, lengths=lengths))
             x = self.norm_layers_1[i](x + y)
             y = self.drop(self.ffn_layers[i](x, x_mask, g=g))
             x = self.norm_layers_2[i](x + y)

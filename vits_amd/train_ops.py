@@ -41,7 +41,7 @@ from torch import nn
 
 from . import _lib
 from ._lib import (EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128, WDT_BF16,
-                   WDT_F16, ConvWgradDesc, check)
+                   WDT_F16, WDT_F32, ConvWgradDesc, check)
 from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
                   layer_norm_channels, layer_norm_channels_backward, make_desc, make_out,
                   weight_norm_effective)
@@ -818,3 +818,69 @@ def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) 
     y = conv1d_hip(x, wp, bias, 1, P - 1 - c0, in_slope, wdt)  # [B, O*u, >= T]
     # phases -> time: y[b][o*u + r][q] -> out[b][o][q*u + r]  (T_out = T*u)
     return y[:, :, :T].reshape(B, O, u, T).permute(0, 1, 3, 2).reshape(B, O, T * u)
+
+
+# ---------------------------------------------------------------------------
+# MultiHeadAttention.attention (attentions.py:85-100) in training
+# ---------------------------------------------------------------------------
+
+
+class AttentionHip(torch.autograd.Function):
+    """out = dropout(softmax(masked_fill(q k^T / sqrt(D), mask == 0, -1e4))) v
+    on [B, H*D, T] channel-major q / k / v (the projection convs' outputs,
+    no transposes), mask = the outer product of the length mask, fp32 MFMA
+    (vits_attention_train_forward / _backward: the forward keeps O and the
+    per-query log-sum-exp, the backward recomputes P).  ``keep`` (uint8 [B,
+    H, T, T] or None) is nn.Dropout's keep mask, applied as keep / (1 - p)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, lengths, heads: int, keep, p: float):
+        B, C, T = q.shape
+        D = C // heads
+        dt = q.dtype
+        code = WDT_F16 if dt == torch.float16 else WDT_F32
+        q, k, v = q.contiguous(), k.to(dt).contiguous(), v.to(dt).contiguous()
+        out = torch.empty_like(q)
+        lse = torch.empty(B, heads, T, device=q.device, dtype=torch.float32)
+        scale = 1.0 / (1.0 - p) if keep is not None else 1.0
+        check(_lib.load().vits_attention_train_forward(
+            q.data_ptr(), k.data_ptr(), v.data_ptr(), None if keep is None else keep.data_ptr(),
+            scale, out.data_ptr(), lse.data_ptr(), B, heads, D, T, lengths.data_ptr(), code,
+            _stream_ptr(q.device)), "vits_attention_train_forward")
+        ctx.save_for_backward(q, k, v, out, lse, lengths, keep)
+        ctx.conf = (heads, D, code, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse, lengths, keep = ctx.saved_tensors
+        heads, D, code, scale = ctx.conf
+        B, C, T = q.shape
+        dout = dout.to(q.dtype).contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        delta = torch.empty(B, heads, T, device=q.device, dtype=torch.float32)
+        check(_lib.load().vits_attention_train_backward(
+            q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
+            None if keep is None else keep.data_ptr(), scale, lse.data_ptr(), delta.data_ptr(),
+            dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, heads, D, T, lengths.data_ptr(), code,
+            _stream_ptr(q.device)), "vits_attention_train_backward")
+        return dq, dk, dv, None, None, None, None
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
+              lengths: torch.Tensor | None, p_drop: float, training: bool):
+    """MultiHeadAttention.attention's output on the HIP training kernels, or
+    None when they do not apply (CPU, no lengths, autocast off, head dim not
+    in 32/64/96/128, q / k / v not of one length): the caller runs torch."""
+    wdt = autocast_wdtype("cuda") if q.device.type == "cuda" else None
+    D = q.shape[1] // heads
+    if (wdt is None or lengths is None or D not in (32, 64, 96, 128) or q.shape != k.shape
+            or k.shape != v.shape or q.dtype not in (torch.float16, torch.float32)):
+        return None
+    keep = None
+    if training and p_drop > 0:
+        B, _, T = q.shape
+        # nn.Dropout's draw: keep with probability 1 - p (device RNG, graph-safe)
+        keep = (torch.rand(B, heads, T, T, device=q.device) >= p_drop).to(torch.uint8)
+    return AttentionHip.apply(q, k, v, lengths.to(torch.int32).contiguous(), heads, keep,
+                              float(p_drop))
