@@ -72,6 +72,8 @@ extern "C" {
 #define VITS_TILE_64x256 1
 #define VITS_TILE_32x256 2
 #define VITS_TILE_64x128 3  /* chosen by the library for small grids of 128x128 layers */
+#define VITS_TILE_128x256 4 /* 16-bit operands with weights from global memory: 2x2  */
+                            /* waves of 64x128 (A fragments feed 4 MFMAs, B 2)      */
 
 typedef struct vits_conv_out {
   float* y;               /* output [B][*][y_cstride]                        */

@@ -171,7 +171,7 @@ struct ConvGroup {
 // half the bytes of the fp32-I/O kernel; accumulation stays fp32.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false,
           bool GA = false>
-__global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
+__global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P || BM * BN >= 128 * 256) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
   static_assert(!IO16 || WT != VITS_WDT_F32, "IO16 needs a 16-bit operand type");
   const int gi = (int)blockIdx.z / G.batch;
   const vits_conv1d_desc& p = G.d[gi];
@@ -1008,51 +1008,63 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
         // trips overlap (res may alias y: each element is still read before
         // it is written, by the same lane).
         if (n < p.n_out) {
-          float v[16];
+          // (in halves of 8 rows on the 128x256 tile: 8 accumulator sub-tiles
+          // are live, so 16-row temporaries would spill)
+          constexpr int RH = TM * TN >= 8 ? 8 : 16;
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            v[r] = apply_act(acc[mi][ni][r] + erow[rloc + (r & 3) + 8 * (r >> 2)], o0.act);
+          for (int r0 = 0; r0 < 16; r0 += RH) {
+          float v[RH];
+#pragma unroll
+          for (int i = 0; i < RH; ++i) {
+            const int r = r0 + i;
+            v[i] = apply_act(acc[mi][ni][r] + erow[rloc + (r & 3) + 8 * (r >> 2)], o0.act);
+          }
           if (p.gmask) {  // leaky-relu derivative of the forward input
             const int64_t gb = (int64_t)b * p.gmask_bstride + n;
-            float gv[16];
+            float gv[RH];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int i = 0; i < RH; ++i) {
+              const int r = r0 + i;
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              gv[r] = ld_io<io_t>(p.gmask, gb + (int64_t)(row < p.m ? row : 0) * p.gmask_cstride);
+              gv[i] = ld_io<io_t>(p.gmask, gb + (int64_t)(row < p.m ? row : 0) * p.gmask_cstride);
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = gv[r] > 0.f ? v[r] : v[r] * p.gmask_slope;
+            for (int i = 0; i < RH; ++i) v[i] = gv[i] > 0.f ? v[i] : v[i] * p.gmask_slope;
           }
           const int64_t yb = (int64_t)b * o0.y_bstride + n;
           if (o0.res) {
             const int64_t rb = (int64_t)b * o0.res_bstride + n;
-            float rv[16];
+            float rv[RH];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int i = 0; i < RH; ++i) {
+              const int r = r0 + i;
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              rv[r] = ld_io<io_t>(o0.res, rb + (int64_t)(row < p.m ? row : 0) * o0.res_cstride);
+              rv[i] = ld_io<io_t>(o0.res, rb + (int64_t)(row < p.m ? row : 0) * o0.res_cstride);
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = rv[r] + o0.res_scale * v[r];
+            for (int i = 0; i < RH; ++i) v[i] = rv[i] + o0.res_scale * v[i];
           }
           if (o0.accumulate) {
-            float yo[16];
+            float yo[RH];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int i = 0; i < RH; ++i) {
+              const int r = r0 + i;
               const int row = rbase + (r & 3) + 8 * (r >> 2);
-              yo[r] = ld_io<io_t>(o0.y, yb + (int64_t)(row < p.m ? row : 0) * o0.y_cstride);
+              yo[i] = ld_io<io_t>(o0.y, yb + (int64_t)(row < p.m ? row : 0) * o0.y_cstride);
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = yo[r] + v[r];
+            for (int i = 0; i < RH; ++i) v[i] = yo[i] + v[i];
           }
           const bool msk = n >= len_b;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
+          for (int i = 0; i < RH; ++i) {
+            const int r = r0 + i;
             const int row = rbase + (r & 3) + 8 * (r >> 2);
-            float t = v[r];
+            float t = v[i];
             if (o0.post_div != 1.0f) t = t / o0.post_div;
             if (msk) t = 0.f;
             if (row < p.m) st_io<io_t>(o0.y, yb + (int64_t)row * o0.y_cstride, t);
+          }
           }
         }
       }
@@ -1175,8 +1187,10 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
     if (e.tile != d.tile || e.epi != d.epi || (e.split < e.m) != (d.split < d.m) ||
         e.wdtype != d.wdtype)
       return VITS_E_UNSUP;
-    const int bm = d.tile == VITS_TILE_128x128 ? 128 : d.tile == VITS_TILE_32x256 ? 32 : 64;
-    const int bn = d.tile == VITS_TILE_64x256 || d.tile == VITS_TILE_32x256 ? 256 : 128;
+    const int bm = (d.tile == VITS_TILE_128x128 || d.tile == VITS_TILE_128x256) ? 128
+                   : d.tile == VITS_TILE_32x256 ? 32 : 64;
+    const int bn = (d.tile == VITS_TILE_64x256 || d.tile == VITS_TILE_32x256 ||
+                    d.tile == VITS_TILE_128x256) ? 256 : 128;
     blocks += (long)((e.n_out + bn - 1) / bn) * ((e.m + bm - 1) / bm) * g.batch;
   }
   switch (d.tile) {
@@ -1209,6 +1223,13 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
     }
     case VITS_TILE_32x256:
       return launch_tile<32, 256, 1, 4, WT, GA>(g, s);
+    case VITS_TILE_128x256:
+      // 16-bit operands on the global-memory weight path only (a 128-row W
+      // stage in LDS would not fit two buffers): 64x128 per wave, so each A
+      // fragment (global) feeds 4 MFMAs and each B fragment (LDS) 2 - half
+      // the vector-memory bytes per MFMA of the 64x64 wave tiles
+      if constexpr (GA) return launch_tile<128, 256, 2, 2, WT, GA>(g, s);
+      return VITS_E_UNSUP;
     default:
       return VITS_E_UNSUP;
   }

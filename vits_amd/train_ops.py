@@ -40,9 +40,9 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from ._lib import (EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128, WDT_BF16,
-                   WDT_F16, WDT_F32, ConvWgradDesc, check)
-from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
+from ._lib import (EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128,
+                   TILE_128x256, WDT_BF16, WDT_F16, WDT_F32, ConvWgradDesc, check)
+from .ops import (T256, PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
                   layer_norm_channels, layer_norm_channels_backward, make_desc, make_out,
                   weight_norm_effective)
 
@@ -59,6 +59,8 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
     k7: 307 -> 377 TF/s)."""
     if m > 32 and n_out is not None and n_out <= 128:
         return TILE_128x128 if (m >= 128 and k <= 5) else TILE_64x128
+    if T256 and m >= 128:
+        return TILE_128x256
     if 64 < m <= 128 and 3 < k <= 7:
         return TILE_64x128
     return _pick_tile_bf16(m, k)
@@ -70,8 +72,10 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
 # MFMA k-step per chunk and waits on every chunk's loads.
 TRAIN_KCK = int(os.environ.get("VITS_TRAIN_KCK", "64"))
 _GA_ALL = os.environ.get("VITS_GA16") == "2"  # weights from global memory: no W LDS budget
-_TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32}
-_TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256}
+_TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32,
+            TILE_128x256: 128}
+_TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256,
+            TILE_128x256: 256}
 
 
 def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
@@ -83,7 +87,8 @@ def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
     xrs = bn + (k - 1) * dil + 8
     xbudget = (6144 if bn <= 128 else 10240) if io16 else (3072 if bn <= 128 else 5120)
     for kc in (64, 48, 32):
-        if (kc * k <= TRAIN_KCK and cin_pad % kc == 0 and (_GA_ALL or kc * k * bm // 2 <= 6144)
+        if (kc * k <= TRAIN_KCK and cin_pad % kc == 0
+                and (_GA_ALL or tile == TILE_128x256 or kc * k * bm // 2 <= 6144)
                 and kc * xrs <= xbudget):
             return kc
     return 16
