@@ -151,6 +151,27 @@ typedef struct vits_conv1d_desc {
   /* bucket; consumers never read past lengths[b] + halo, halo < len_skip,  */
   /* and [lengths[b], lengths[b] + len_skip) is written as zeros); 0 = off  */
   int32_t len_skip;
+  /* row-joined 2-D convs (the STFT discriminators' Conv2d(C, O, (k0, k1),   */
+  /* stride (s0, 1), padding (0, p1)), mrd.py:122-133, as a 1-D conv over   */
+  /* frequency rows laid end to end in padded rows of L columns: [B][C][F] */
+  /* [L], L = T + 2 p1 rounded up to 4, zeros in each row's pad columns).    */
+  /* x_rowlen = L > 0: window column n of x is read at (n / L) * x_rowmul + */
+  /* n % L (x_rowmul = s0 * L: output row f reads input rows s0 f + i);     */
+  /* x_cgroup > 0: virtual channel v = i * x_cgroup + c (frequency tap i,    */
+  /* real channel c) is read at c * x_cstride + i * x_gstride (a K-chunk    */
+  /* must not straddle two taps when x_cgroup >= kc).  y_rowlen = L > 0:    */
+  /* output column n is written at (n / L) * y_rowmul + n % L, and as 0     */
+  /* where n % L lies outside [y_rowpad, y_rowpad + y_rowvalid) (the pad   */
+  /* columns the next layer reads as its zero padding); gmask / res use    */
+  /* the output's column map.  All 0 = plain 1-D conv.                      */
+  int32_t x_rowlen;
+  int32_t x_rowmul;
+  int32_t x_cgroup;
+  int32_t x_gstride;
+  int32_t y_rowlen;
+  int32_t y_rowmul;
+  int32_t y_rowpad;
+  int32_t y_rowvalid;
 } vits_conv1d_desc;
 
 #define VITS_WDT_F32 0
@@ -437,6 +458,13 @@ typedef struct vits_conv1d_wgrad_desc {
   int32_t io16;           /* dy / x are tensors of the 16-bit operand type   */
                           /* (strides in elements)                           */
   int32_t reserved2;
+  /* row-joined 2-D layers (see vits_conv1d_desc.x_rowlen): x column t at */
+  /* (t / x_rowlen) * x_rowmul + t % x_rowlen, virtual channel v = i *     */
+  /* x_cgroup + c at c * x_cstride + i * x_gstride; dy plain; 0 = off      */
+  int32_t x_rowlen;
+  int32_t x_rowmul;
+  int32_t x_cgroup;
+  int32_t x_gstride;
 } vits_conv1d_wgrad_desc;
 /* dW[co][ci][j] = sum_{b,t} dY[b][co][t] * act(x[b][ci][t - pad_left + j*dil]) */
 /* (operands rounded to wdtype, fp32 accumulation; VITS_E_UNSUP when       */

@@ -47,13 +47,14 @@ def test_struct_layout_matches_header():
 #include <stdio.h>
 #include <stddef.h>
 #include "vits_amd.h"
-int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu %zu %zu\n", sizeof(vits_conv1d_desc),
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc),
  sizeof(vits_conv_out), offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths),
  offsetof(vits_conv1d_desc, wdtype), sizeof(vits_stft_job), offsetof(vits_stft_job, eps),
  sizeof(vits_resblock_pair_desc), offsetof(vits_resblock_pair_desc, w2),
  offsetof(vits_resblock_pair_desc, post_div), sizeof(vits_wnorm_layer),
  sizeof(vits_snorm_layer), offsetof(vits_snorm_layer, eps), VITS_WNORM_MAX, VITS_SNORM_MAX,
- sizeof(vits_pack16_layer), offsetof(vits_pack16_layer, img_t), offsetof(vits_pack16_layer, cin_pad_t));
+ sizeof(vits_pack16_layer), offsetof(vits_pack16_layer, img_t), offsetof(vits_pack16_layer, cin_pad_t),
+ offsetof(vits_conv1d_desc, x_rowlen), offsetof(vits_conv1d_desc, y_rowvalid));
  return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -80,3 +81,5 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu
     assert int(out[15]) == ctypes.sizeof(Pack16Layer)
     assert int(out[16]) == Pack16Layer.img_t.offset
     assert int(out[17]) == Pack16Layer.cin_pad_t.offset
+    assert int(out[18]) == ConvDesc.x_rowlen.offset
+    assert int(out[19]) == ConvDesc.y_rowvalid.offset

@@ -541,3 +541,46 @@ def test_attention_train_dropout_statistics(device):
         yb = train_ops.attention(q, k, v, H, lengths, 0.1, training=True)
         yc = train_ops.attention(q, k, v, H, lengths, 0.1, training=True)
     assert torch.equal(ya, yb) and not torch.equal(ya, yc) and not torch.equal(ya, y0)
+
+
+@pytest.mark.parametrize("C,O,k0,s0,k1,F,T,slope", [(64, 64, 5, 2, 5, 65, 289, 0.2),
+                                                    (64, 64, 5, 2, 5, 13, 19, 0.2),
+                                                    (64, 64, 5, 2, 5, 30, 37, 1.0),
+                                                    (64, 1, 1, 1, 1, 1, 73, 0.2)])
+def test_conv2d_rows_fwd_bwd(device, C, O, k0, s0, k1, F, T, slope):
+    """train_ops.Conv2dRowsHip16 (an STFT-discriminator Conv2d(C, O, (k0,
+    k1), stride (s0, 1), padding (0, k1 // 2)) of leaky_relu(x) as one
+    row-joined conv on the row-padded layout, mrd.py:122-133) against torch
+    conv2d in fp32 on the same fp16-rounded operands: y, dx, dW, db within
+    2e-3 of each tensor's max (fp16 outputs); the pad rows / columns of y
+    and dx are exactly zero."""
+    torch.manual_seed(7)
+    B, p1, lp = 3, k1 // 2, 2
+    R = train_ops.ROW_PAD
+    L = train_ops.rows_len(T, lp)
+    x = torch.randn(B, C, F, T, device=device).half()
+    w = (torch.randn(O, C, k0, k1, device=device) * 0.05)
+    bias = torch.randn(O, device=device) * 0.1
+    xp = F_.pad(x, (lp, L - T - lp, R, R)).requires_grad_(True)
+    wa, ba = w.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+    y = train_ops.Conv2dRowsHip16.apply(xp, wa, ba, s0, p1, lp, T, slope, train_ops.WDT_F16)
+    F_out = (F - k0) // s0 + 1
+    assert y.shape == (B, O, F_out + 2 * R, L) and y.dtype == torch.float16
+    gy = torch.randn(B, O, F_out, T, device=device).half()
+    gyp = F_.pad(gy, (lp, L - T - lp, R, R))
+    y.backward(gyp)
+    # reference: fp32 torch on the rounded operands
+    xr = x.float().requires_grad_(True)
+    wr = w.half().float().requires_grad_(True)
+    br = bias.clone().requires_grad_(True)
+    yr = F_.conv2d(F_.leaky_relu(xr, slope) if slope != 1.0 else xr, wr, br, stride=(s0, 1),
+                   padding=(0, p1))
+    yr.backward(gy.float())
+    yv = y[:, :, R:R + F_out, lp:lp + T].float()
+    assert (y.float().abs().sum() - yv.abs().sum()).abs().item() == 0  # pads are zero
+    dxv = xp.grad[:, :, R:R + F, lp:lp + T].float()
+    assert (xp.grad.float().abs().sum() - dxv.abs().sum()).abs().item() == 0
+    for got, want, what in ((yv, yr, "y"), (dxv, xr.grad, "dx"), (wa.grad, wr.grad, "dw"),
+                            (ba.grad, br.grad, "db")):
+        err = (got.float() - want).abs().max().item() / want.abs().max().item()
+        assert err <= 2e-3, (what, err)

@@ -82,6 +82,14 @@ class ConvDesc(C.Structure):
         ("gmask_slope", C.c_float),
         ("io16", C.c_int32),
         ("len_skip", C.c_int32),
+        ("x_rowlen", C.c_int32),
+        ("x_rowmul", C.c_int32),
+        ("x_cgroup", C.c_int32),
+        ("x_gstride", C.c_int32),
+        ("y_rowlen", C.c_int32),
+        ("y_rowmul", C.c_int32),
+        ("y_rowpad", C.c_int32),
+        ("y_rowvalid", C.c_int32),
     ]
 
 
@@ -160,6 +168,10 @@ class ConvWgradDesc(C.Structure):
         ("reserved", C.c_int32),
         ("io16", C.c_int32),
         ("reserved2", C.c_int32),
+        ("x_rowlen", C.c_int32),
+        ("x_rowmul", C.c_int32),
+        ("x_cgroup", C.c_int32),
+        ("x_gstride", C.c_int32),
     ]
 
 

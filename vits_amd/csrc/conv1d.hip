@@ -52,6 +52,16 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   if (d.wdtype != VITS_WDT_F32) VITS_CHECK_SHAPE((d.kc % 16) == 0);
   if (d.gmask) VITS_CHECK_ARG(d.epi == VITS_EPI_STORE && d.split >= d.m);
   if (d.io16) VITS_CHECK_ARG(d.wdtype == VITS_WDT_BF16 || d.wdtype == VITS_WDT_F16);
+  // row-joined 2-D layers: 4-column blocks within one row, single-output
+  // STORE, K-chunks inside one frequency tap
+  VITS_CHECK_ARG(d.x_rowlen >= 0 && d.y_rowlen >= 0 && d.x_cgroup >= 0);
+  if (d.x_rowlen) VITS_CHECK_SHAPE((d.x_rowlen & 3) == 0 && d.x_rowmul >= d.x_rowlen &&
+                                   d.x_tstride == 1);
+  if (d.x_cgroup) VITS_CHECK_SHAPE(d.x_cgroup % d.kc == 0);
+  if (d.y_rowlen)
+    VITS_CHECK_ARG(d.epi == VITS_EPI_STORE && d.split >= d.m && d.y_rowmul >= d.y_rowlen &&
+                   d.y_rowpad >= 0 && d.y_rowvalid >= 0 &&
+                   d.y_rowpad + d.y_rowvalid <= d.y_rowlen);
   return VITS_OK;
 }
 

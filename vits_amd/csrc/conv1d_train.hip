@@ -132,6 +132,23 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
   // VEC window: rows from the 4-aligned start t0 - pad_left - sh
   const int sh = VEC ? ((p.pad_left & 3) ? 4 - (p.pad_left & 3) : 0) : 0;
 
+  // x addressing (row-joined 2-D layers, vits_conv1d_wgrad_desc.x_rowlen):
+  // virtual channel v -> row base, window column t -> offset in the row
+  auto vbase = [&](int v) -> int64_t {
+    if (p.x_cgroup > 0) {
+      const int i = v / p.x_cgroup;
+      return (int64_t)(v - i * p.x_cgroup) * p.x_cstride + (int64_t)i * p.x_gstride;
+    }
+    return (int64_t)v * p.x_cstride;
+  };
+  auto xcol = [&](int t) -> int {
+    if (p.x_rowlen > 0) {
+      const int f = t / p.x_rowlen;
+      return f * p.x_rowmul + (t - f * p.x_rowlen);
+    }
+    return t;
+  };
+
   typedef typename Op16<WT>::T T16;
   typedef T16 t16x4 __attribute__((ext_vector_type(4)));
   t16x4 dyr[IO16 ? 4 : 1], xr[IO16 ? 8 : 1];  // raw IO16 blocks
@@ -169,7 +186,7 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
       for (int e = 0; e < 2; ++e) {
         t16x4 v = {};
         if (tok && ci + e < p.cin)
-          v = *reinterpret_cast<const t16x4*>(xb + (int64_t)(ci + e) * p.x_cstride + t);
+          v = *reinterpret_cast<const t16x4*>(xb + vbase(ci + e) + xcol(t));
         xr[2 * q + e] = v;
       }
     }
@@ -225,7 +242,7 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
       for (int e = 0; e < 2; ++e) {
         f32x4v v = {0.f, 0.f, 0.f, 0.f};
         if (tok && ci + e < p.cin)
-          v = *reinterpret_cast<const f32x4v*>(xb + (int64_t)(ci + e) * p.x_cstride + t);
+          v = *reinterpret_cast<const f32x4v*>(xb + vbase(ci + e) + xcol(t));
 #pragma unroll
         for (int i = 0; i < 4; ++i) xv[8 * q + 4 * e + i] = v[i];
       }
@@ -292,7 +309,7 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const bool ok = tok && ci + e < p.cin;
-          xh[(i * 2 + h) * 2 + e] = ok ? xb[(int64_t)(ci + e) * p.x_cstride + t] : (el_t)0.f;
+          xh[(i * 2 + h) * 2 + e] = ok ? xb[vbase(ci + e) + xcol(t)] : (el_t)0.f;
         }
       }
     }
@@ -527,6 +544,8 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
                    (reinterpret_cast<uintptr_t>(d.dy) & al) == 0 && (d.x_cstride & 3) == 0 &&
                    (d.x_bstride & 3) == 0 && (reinterpret_cast<uintptr_t>(d.x) & al) == 0 &&
                    (d.tin & 3) == 0 && KT + (d.k - 1) * d.dil + sh <= MAX_WR &&
+                   (d.x_rowlen == 0 ||
+                    ((d.x_rowlen & 3) == 0 && (d.x_rowmul & 3) == 0 && (d.x_gstride & 3) == 0)) &&
                    (d.k > 1 || d.io16);  // k = 1 (tools/wgrad_split_bench.py: 40 -> 53 us)
                                          // keeps the element-wise map for fp32 inputs
   switch (d.k) {

@@ -115,6 +115,27 @@ class STFTDiscriminator(nn.Module):
             # conv kernel in the step) on the HIP training conv
             h = conv2d_freq(first, h, wdt)
             layers = layers[1:]
+        if (STFT_D_HIP and STFT_D_ROWS and wdt is not None and train_ops._io16(wdt) and layers
+                and h.dim() == 4 and _rows_ok(layers)):
+            # every remaining layer as one row-joined HIP conv on the
+            # row-padded layout (train_ops.Conv2dRowsHip16), the LeakyReLU
+            # between two layers fused into the next conv's input staging
+            T = h.shape[3]
+            lp = max(l.padding[1] for l in layers if isinstance(l, Conv2d))
+            L = train_ops.rows_len(T, lp)
+            R = train_ops.ROW_PAD
+            hp = torch.nn.functional.pad(h.to(train_ops._TORCH_16[wdt]), (lp, L - T - lp, R, R))
+            slope = 1.0
+            for layer in layers:
+                if isinstance(layer, LeakyReLU):
+                    slope = layer.negative_slope
+                    continue
+                w = layer.weight
+                hp = train_ops.Conv2dRowsHip16.apply(hp, w, layer.bias, layer.stride[0],
+                                                     layer.padding[1], lp, T, slope, wdt)
+                slope = 1.0
+            assert hp.shape[1] == 1 and hp.shape[2] == 1 + 2 * R
+            return hp[:, 0, R, lp:lp + T]
         if STFT_D_HIP_ALL and wdt is not None and layers and all(
                 _freq_conv_ok(l) for l in layers if isinstance(l, Conv2d)):
             # every remaining layer on the HIP training conv, the LeakyReLU
@@ -144,6 +165,24 @@ class STFTDiscriminator(nn.Module):
 
 
 STFT_D_HIP = True  # test switch: False keeps every STFT-discriminator conv on torch
+# layers 2+ as row-joined HIP convs on the row-padded layout (train_ops.Conv2dRowsHip16)
+STFT_D_ROWS = os.environ.get("VITS_STFT_D_ROWS", "1") != "0"
+
+
+def _rows_ok(layers) -> bool:
+    """Conv2d layers of Conv2dRowsHip16's form: groups 1, dilation 1, time
+    stride 1, no frequency padding, 'same' time padding (k1 = 2 p1 + 1),
+    k1 on the conv kernel's tap list, 64-multiple channel counts (K-chunks
+    within one frequency tap) - except the last layer's single output."""
+    convs = [l for l in layers if isinstance(l, Conv2d)]
+    lp = max(l.padding[1] for l in convs)
+    for l in convs:
+        if (l.groups != 1 or l.dilation != (1, 1) or l.stride[1] != 1 or l.padding[0] != 0
+                or 2 * l.padding[1] + 1 != l.kernel_size[1] or l.padding_mode != "zeros"
+                or l._forward_pre_hooks or l.in_channels % 16 != 0
+                or not train_ops._lib_k_ok(l.kernel_size[1], 1)):
+            return False
+    return lp >= 1
 # all STFT-discriminator layers (not only the first) on the HIP conv
 STFT_D_HIP_ALL = os.environ.get("VITS_STFT_D_HIP_ALL", "0") != "0"
 # channels-last operands for the STFT discriminators' MIOpen convs: its NHWC
@@ -240,7 +279,7 @@ class GroupedSpectralNorm:
         # first, which conv2d_freq lowers onto the HIP conv): their W / sigma
         # is produced as the fp16 channels-last operand under autocast
         firsts = {id(sub.convs[0]) for sub in root.modules() if isinstance(sub, STFTDiscriminator)}
-        cl = (STFT_D_NHWC and not STFT_D_HIP_ALL
+        cl = (STFT_D_NHWC and not STFT_D_HIP_ALL and not STFT_D_ROWS
               and os.environ.get("VITS_SN_CL", "1") != "0")  # A/B switch
         self.cl16 = [cl and isinstance(m, Conv2d) and id(m) not in firsts for m, _, _ in self.flat]
 

@@ -889,3 +889,149 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
         keep = (torch.rand(B, heads, T, T, device=q.device) >= p_drop).to(torch.uint8)
     return AttentionHip.apply(q, k, v, lengths.to(torch.int32).contiguous(), heads, keep,
                               float(p_drop))
+
+
+# ---------------------------------------------------------------------------
+# STFT-discriminator Conv2d layers (mrd.py:122-133) on the HIP training conv
+# ---------------------------------------------------------------------------
+# Row-padded layout of the activations between the layers: [B, C, F + 4, L],
+# frequency rows f at row f + 2 (two zero rows at each end: the input
+# gradient's phase convs read two rows past either end), time t at column
+# p1 + t of an L = round_up(T + 2 p1, 4) row (zeros in the pad columns:
+# the next layer's zero padding along time).  Every layer is ONE row-joined
+# conv (vits_conv1d_desc.x_rowlen / x_cgroup / y_rowlen): columns n = f_out
+# * L + t, virtual input channels v = i * C + c (frequency tap i), k1 time
+# taps; output row f_out reads input rows s0 * f_out + i.
+ROW_PAD = 2
+
+
+def rows_len(T: int, p1: int) -> int:
+    return (T + 2 * p1 + 3) // 4 * 4
+
+
+def _pack16_img(w3: torch.Tensor, transpose: bool, wdtype: int) -> torch.Tensor:
+    """16-bit image of a [cout][cin][k] fp32 weight (vits_conv1d_pack16)."""
+    cout, cin, k = w3.shape
+    rows, chans = (cin, cout) if transpose else (cout, cin)
+    m_pad, cin_pad = (rows + 127) // 128 * 128, (chans + 15) // 16 * 16
+    img = torch.empty(cin_pad // 16, k, 2, m_pad, 8, dtype=_TORCH_16[wdtype], device=w3.device)
+    check(_lib.load().vits_conv1d_pack16(
+        w3.data_ptr(), cout, cin, k, int(transpose), img.data_ptr(), m_pad, cin_pad, wdtype,
+        None, 0, _stream_ptr(w3.device)), "vits_conv1d_pack16")
+    return img
+
+
+def _rows_desc(img, wdtype, rows, chans, k, pad_left, x, x_off, x_cstride, x_bstride, x_rowmul,
+               x_cgroup, x_gstride, L, n_rows_out, y, y_off, y_cstride, y_bstride, y_rowmul,
+               lp, T, in_slope, bias=None, gmask=None, gmask_off=0, gmask_slope=1.0):
+    tile = _pick_tile_train(rows, k, n_rows_out * L)
+    kc = _train_kc(img.shape[0] * 16, k, 1, tile, True)
+    while x_cgroup % kc:
+        kc //= 2
+    d = _lib.ConvDesc()
+    d.x = x.data_ptr() + x.element_size() * x_off
+    d.io16 = 1
+    d.x_bstride, d.x_cstride, d.x_tstride = x_bstride, x_cstride, 1
+    d.cin = chans
+    d.tin = n_rows_out * L
+    d.in_slope = in_slope
+    d.w = img.data_ptr()
+    d.m, d.m_pad, d.cin_pad, d.kc = rows, img.shape[3], img.shape[0] * 16, kc
+    d.k, d.dil, d.pad_left = k, 1, pad_left
+    d.n_out = n_rows_out * L
+    d.tile, d.epi = tile, EPI_STORE
+    d.bias = None if bias is None else bias.data_ptr()
+    d.split = rows
+    d.lengths = None
+    d.out0 = make_out(y)
+    d.out0.y = y.data_ptr() + y.element_size() * y_off
+    d.out0.y_bstride, d.out0.y_cstride = y_bstride, y_cstride
+    d.out1 = make_out(y)
+    d.wdtype = wdtype
+    if gmask is not None:
+        d.gmask = gmask.data_ptr() + gmask.element_size() * gmask_off
+        d.gmask_bstride, d.gmask_cstride = gmask.stride(0), gmask.stride(1)
+        d.gmask_slope = gmask_slope
+    d.x_rowlen, d.x_rowmul, d.x_cgroup, d.x_gstride = L, x_rowmul, x_cgroup, x_gstride
+    d.y_rowlen, d.y_rowmul, d.y_rowpad, d.y_rowvalid = L, y_rowmul, lp, T
+    return d
+
+
+class Conv2dRowsHip16(torch.autograd.Function):
+    """Conv2d(C, O, (k0, k1), stride (s0, 1), padding (0, p1)) of
+    leaky_relu(x, in_slope) on the row-padded fp16 layout (see ROW_PAD; lp =
+    the layout's pad columns, >= p1; T valid columns per row):
+    x [B, C, F + 4, L] -> y [B, O, F_out + 4, L], F_out = (F - k0) // s0 + 1.
+    Forward: one row-joined conv over virtual channels (i, c).  Input
+    gradient: s0 phase convs (input rows s0 q + rho take the taps i = rho +
+    s0 i', reading output-gradient rows q - i'), the leaky-relu derivative of
+    x in their epilogue.  Weight / bias gradient: the row-joined split-K
+    wgrad over (b, f_out, t).  fp16 operands, fp32 accumulation, dW fp32."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, s0: int, p1: int, lp: int, T: int, in_slope: float,
+                wdtype: int):
+        B, C, Fp, L = x.shape
+        F_ = Fp - 2 * ROW_PAD
+        O, _, k0, k1 = weight.shape
+        F_out = (F_ - k0) // s0 + 1
+        w32 = weight.detach().float()
+        wv = w32.permute(0, 2, 1, 3).reshape(O, k0 * C, k1).contiguous()  # v = i * C + c
+        img = _pack16_img(wv, False, wdtype)
+        y = torch.zeros(B, O, F_out + 2 * ROW_PAD, L, device=x.device, dtype=x.dtype)
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        d = _rows_desc(img, wdtype, O, k0 * C, k1, p1, x, ROW_PAD * L, Fp * L, C * Fp * L,
+                       s0 * L, C, L, L, F_out, y, ROW_PAD * L, y.stride(1), y.stride(0), L, lp,
+                       T, in_slope, bias=b32)
+        conv1d_launch(d, B, x.device)
+        ctx.save_for_backward(x, w32)
+        ctx.conf = (s0, p1, lp, T, in_slope, wdtype, bias is not None, F_out)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w32 = ctx.saved_tensors
+        s0, p1, lp, T, slope, wdtype, has_bias, F_out = ctx.conf
+        B, C, Fp, L = x.shape
+        F_ = Fp - 2 * ROW_PAD
+        O, _, k0, k1 = w32.shape
+        dy = dy.to(x.dtype).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.zeros_like(x)
+            for rho in range(s0):
+                taps = list(range(rho, k0, s0))            # i = rho + s0 * i'
+                Q = (F_ - rho + s0 - 1) // s0               # input rows s0 q + rho < F
+                if not taps or Q <= 0:
+                    continue
+                # [(i', o)][c][j] -> rows c, virtual channels (i', o), taps reversed
+                wp = w32[:, :, taps, :].permute(2, 0, 1, 3).reshape(len(taps) * O, C, k1)
+                img = _pack16_img(wp.contiguous(), True, wdtype)
+                d = _rows_desc(img, wdtype, C, len(taps) * O, k1, k1 - 1 - p1, dy, ROW_PAD * L,
+                               dy.stride(1), dy.stride(0), L, O, -L, L, Q, dx,
+                               (ROW_PAD + rho) * L, dx.stride(1), dx.stride(0), s0 * L, lp, T, 1.0,
+                               gmask=x if slope != 1.0 else None,
+                               gmask_off=(ROW_PAD + rho) * L, gmask_slope=slope)
+                conv1d_launch(d, B, x.device)
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dwv = torch.empty(O, k0 * C, k1, device=x.device, dtype=torch.float32)
+            db = torch.empty(O, device=x.device, dtype=torch.float32) if has_bias else None
+            wd = _lib.ConvWgradDesc()
+            wd.dy = dy.data_ptr() + dy.element_size() * ROW_PAD * L
+            wd.dy_bstride, wd.dy_cstride, wd.cout = dy.stride(0), dy.stride(1), O
+            wd.x = x.data_ptr() + x.element_size() * ROW_PAD * L
+            wd.x_bstride, wd.x_cstride, wd.cin = x.stride(0), x.stride(1), k0 * C
+            wd.tin, wd.n_out, wd.k, wd.dil, wd.pad_left = F_out * L, F_out * L, k1, 1, p1
+            wd.in_slope = slope
+            wd.dw_t = dwv.data_ptr()
+            wd.dbias = None if db is None else db.data_ptr()
+            wd.wdtype = wdtype
+            wd.io16 = 1
+            wd.x_rowlen, wd.x_rowmul, wd.x_cgroup, wd.x_gstride = L, s0 * L, C, L
+            lib = _lib.load()
+            nws = int(lib.vits_conv1d_wgrad_workspace(wd, B))
+            ws = torch.empty(max(nws, 1), device=x.device, dtype=torch.float32)
+            check(lib.vits_conv1d_wgrad_split(wd, B, ws.data_ptr(), nws, _stream_ptr(x.device)),
+                  "vits_conv1d_wgrad_split")
+            dw = dwv.view(O, k0, C, k1).permute(0, 2, 1, 3).contiguous()
+        return dx, dw, db, None, None, None, None, None, None
