@@ -59,6 +59,9 @@ extern "C" {
 /* epilogue kinds */
 #define VITS_EPI_STORE 0     /* y = act(acc + bias + cond) [+res] [accumulate] */
 #define VITS_EPI_GATE 1      /* y[p] = tanh(v[2p]) * sigmoid(v[2p+1])           */
+                             /* (+ out1.y set: the pre-activation acc + bias,   */
+                             /* no cond, to out1 channels p and m/2 + p - the   */
+                             /* training gate's saved input)                    */
 #define VITS_EPI_UPSAMPLE 2  /* polyphase ConvTranspose1d output scatter        */
 
 /* activations applied to v before residual/accumulate (STORE epilogue) */
@@ -432,6 +435,8 @@ typedef struct vits_pack16_layer {
   int32_t m_pad, cin_pad;
   void* img_t;      /* [cin_pad_t/16][k][2][m_pad_t][8], rows cin, taps reversed */
   int32_t m_pad_t, cin_pad_t;
+  int32_t gate;     /* 1: img rows gate-interleaved (row 2q = output q, row 2q+1 = */
+                    /* output cout/2 + q: VITS_EPI_GATE); img_t stays natural      */
 } vits_pack16_layer;
 int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, int wdtype, void* stream);
 

@@ -584,3 +584,43 @@ def test_conv2d_rows_fwd_bwd(device, C, O, k0, s0, k1, F, T, slope):
                             (ba.grad, br.grad, "db")):
         err = (got.float() - want).abs().max().item() / want.abs().max().item()
         assert err <= 2e-3, (what, err)
+
+
+@pytest.mark.parametrize("cin,H,k,dil,T,slope,with_g", [(64, 64, 5, 1, 500, 1.0, True),
+                                                        (64, 32, 7, 3, 384, 0.1, True),
+                                                        (48, 40, 3, 1, 130, 1.0, False)])
+def test_conv_gate_fused_matches_conv_then_gate(device, cin, H, k, dil, T, slope, with_g):
+    """train_ops.conv1d_gate (one conv launch: GATE epilogue on gate-
+    interleaved weight rows + the pre-activation output for the backward)
+    against the unfused conv1d -> GateHip16 path on the same inputs under
+    fp16 autocast: acts and the gradients of x, W, b, g agree to 2e-3 of each
+    tensor's max (the fused gate reads the fp32 accumulator instead of the
+    fp16-rounded conv output), and the pre-activation it saves equals the
+    unfused conv output to fp16 rounding."""
+    torch.manual_seed(4)
+    B = 2
+    conv = torch.nn.Conv1d(cin, 2 * H, k, dilation=dil, padding=dil * (k - 1) // 2).to(device)
+    conv._vits_gate = True
+    x = torch.randn(B, cin, T, device=device)
+    g = torch.randn(B, 2 * H, device=device) if with_g else None
+    gy = torch.randn(B, H, T, device=device)
+
+    def run(fused):
+        for p in conv.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        gi = None if g is None else g.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.float16):
+            if fused:
+                y = train_ops.conv1d_gate(conv, xi, gi, in_slope=slope)
+                assert y is not None
+            else:
+                y = train_ops.gate(train_ops.conv1d(conv, xi, in_slope=slope), gi)
+        y.float().backward(gy)
+        return [y.float(), xi.grad, conv.weight.grad, conv.bias.grad] + (
+            [gi.grad.float()] if gi is not None else [])
+
+    a, b = run(False), run(True)
+    for i, (u, v) in enumerate(zip(a, b)):
+        err = (u.float() - v.float()).abs().max().item() / u.float().abs().max().item()
+        assert err <= 2e-3, (i, err)

@@ -204,6 +204,7 @@ class Pack16Layer(C.Structure):
         ("img_t", C.c_void_p),
         ("m_pad_t", C.c_int32),
         ("cin_pad_t", C.c_int32),
+        ("gate", C.c_int32),
     ]
 
 

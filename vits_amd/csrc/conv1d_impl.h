@@ -947,17 +947,22 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P ||
   // rows, fetched once by BM threads in parallel into LDS (the stages are
   // free after the last barrier of the K loop)
   float* const erow = smem;
+  // GATE with a pre-activation output (out1.y: the training gate's saved
+  // input, bias but no cond, as the reference's in_layer output x_in)
+  float* const ebias = smem + BM;
+  const bool gate_pre = EPI == VITS_EPI_GATE && p.out1.y != nullptr;
   if (tid < BM) {
     const int row = m0 + tid;
-    float e = 0.f;
+    float e = 0.f, eb = 0.f;
     if (row < p.m) {
       int idx = row;
       if (EPI == VITS_EPI_GATE) idx = (row & 1) ? (p.m >> 1) + (row >> 1) : (row >> 1);
       if (EPI == VITS_EPI_UPSAMPLE) idx = row / p.up_u;
-      if (p.bias) e = p.bias[idx];
+      if (p.bias) eb = e = p.bias[idx];
       if (cond && EPI != VITS_EPI_UPSAMPLE) e += cond[idx];
     }
     erow[tid] = e;
+    if (EPI == VITS_EPI_GATE) ebias[tid] = eb;
   }
   __syncthreads();
 
@@ -981,6 +986,15 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P ||
               const float vb = acc[mi][ni][r + 1] + erow[rloc + ro + 1];
               const float v = fast_tanh(va) * fast_sigmoid(vb);
               store_std<io_t>(o0, b, row >> 1, n, v, n >= len_b);
+              if (gate_pre) {
+                const bool mk = n >= len_b;
+                const int64_t pb = (int64_t)b * p.out1.y_bstride + n;
+                const float xa = mk ? 0.f : acc[mi][ni][r] + ebias[rloc + ro];
+                const float xb = mk ? 0.f : acc[mi][ni][r + 1] + ebias[rloc + ro + 1];
+                st_io<io_t>(p.out1.y, pb + (int64_t)(row >> 1) * p.out1.y_cstride, xa);
+                st_io<io_t>(p.out1.y, pb + (int64_t)((p.m >> 1) + (row >> 1)) * p.out1.y_cstride,
+                            xb);
+              }
             }
           }
         }

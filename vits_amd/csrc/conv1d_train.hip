@@ -585,7 +585,7 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
 template <typename T>
 __device__ __forceinline__ void pack16_elem(const float* __restrict__ w, int cout, int cin, int k,
                                             int transpose, T* __restrict__ out, int m_pad,
-                                            int64_t i) {
+                                            int64_t i, int gate = 0) {
   const int c8 = (int)(i & 7);
   int64_t r = i >> 3;
   const int m = (int)(r % m_pad);
@@ -597,7 +597,9 @@ __device__ __forceinline__ void pack16_elem(const float* __restrict__ w, int cou
   const int c = cg * 16 + half * 8 + c8;
   float v = 0.f;
   if (!transpose) {
-    if (m < cout && c < cin) v = w[((int64_t)m * cin + c) * k + j];
+    // gate-interleaved rows (VITS_EPI_GATE): row 2q = output q, 2q+1 = cout/2 + q
+    const int src = gate ? ((m & 1) ? (cout >> 1) + (m >> 1) : (m >> 1)) : m;
+    if (m < cout && c < cin) v = w[((int64_t)src * cin + c) * k + j];
   } else {
     if (m < cin && c < cout) v = w[((int64_t)c * cin + m) * k + (k - 1 - j)];
   }
@@ -641,7 +643,8 @@ __global__ __launch_bounds__(256) void pack16_pairs_kernel(const PackList L) {
     const int64_t total = (int64_t)e.cin_pad * e.k * e.m_pad;
     const int64_t r = i - L.start[q];
     if (r < total)
-      pack16_elem<T>(e.w, e.cout, e.cin, e.k, 0, reinterpret_cast<T*>(e.img), e.m_pad, r);
+      pack16_elem<T>(e.w, e.cout, e.cin, e.k, 0, reinterpret_cast<T*>(e.img), e.m_pad, r,
+                     e.gate);
     else
       pack16_elem<T>(e.w, e.cout, e.cin, e.k, 1, reinterpret_cast<T*>(e.img_t), e.m_pad_t,
                      r - total);
@@ -805,6 +808,7 @@ extern "C" int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, 
     for (int q = 0; q < L.n; ++q) {
       const vits_pack16_layer& e = layers[b0 + q];
       VITS_CHECK_ARG(e.w && e.img && e.img_t && e.cout > 0 && e.cin > 0 && e.k > 0);
+      VITS_CHECK_ARG(e.gate == 0 || (e.gate == 1 && (e.cout & 1) == 0));
       VITS_CHECK_SHAPE(e.m_pad % 128 == 0 && e.m_pad >= e.cout && e.cin_pad % 16 == 0 &&
                        e.cin_pad >= e.cin);
       VITS_CHECK_SHAPE(e.m_pad_t % 128 == 0 && e.m_pad_t >= e.cin && e.cin_pad_t % 16 == 0 &&

@@ -66,6 +66,7 @@ class WN(nn.Module):
             self.in_layers.append(weight_norm(
                 nn.Conv1d(hidden_channels, 2 * hidden_channels, kernel_size, dilation=dilation,
                           padding=padding)))
+            self.in_layers[-1]._vits_gate = True  # feeds only the gate (train_ops.conv1d_gate)
             rs = 2 * hidden_channels if i < n_layers - 1 else hidden_channels
             self.res_skip_layers.append(weight_norm(nn.Conv1d(hidden_channels, rs, 1)))
 
@@ -80,8 +81,15 @@ class WN(nn.Module):
             g = train_ops.linear(self.cond_layer, g)
         x16 = None  # x rounded to the conv dtype by the fused update (WNUpdate16)
         for i in range(self.n_layers):
-            x_in = train_ops.conv1d(self.in_layers[i], x if x16 is None else x16)
-            acts = self.drop(self._gate(x_in, g if self.gin_channels else None, i))
+            xi = x if x16 is None else x16
+            H2 = 2 * H
+            g_l = g[:, i * H2:(i + 1) * H2] if self.gin_channels else None
+            # in_layer conv + gate as one launch on the fp16 training path
+            acts = train_ops.conv1d_gate(self.in_layers[i], xi, g_l)
+            if acts is None:
+                acts = self._gate(train_ops.conv1d(self.in_layers[i], xi),
+                                  g if self.gin_channels else None, i)
+            acts = self.drop(acts)
             rs = train_ops.conv1d(self.res_skip_layers[i], acts)
             if i < self.n_layers - 1:
                 # x = (x + rs[:, :H]) * x_mask ; output = output + rs[:, H:]
@@ -114,6 +122,8 @@ class ResBlock2(nn.Module):
         self.convs1 = nn.ModuleList([
             weight_norm(nn.Conv1d(channels, inter, kernel_size, 1, dilation=d,
                                   padding=get_padding(kernel_size, d))) for d in dilation])
+        for c in self.convs1:
+            c._vits_gate = True  # feeds only the gate (train_ops.conv1d_gate)
         self.convs2 = nn.ModuleList([
             weight_norm(nn.Conv1d(inter // 2, channels, kernel_size, 1, dilation=1,
                                   padding=get_padding(kernel_size, 1))) for _ in dilation])
@@ -130,8 +140,11 @@ class ResBlock2(nn.Module):
 
             return resblock_infer(self, x, g)
         for i, (c1, c2, cs) in enumerate(zip(self.convs1, self.convs2, self.conds)):
-            xt = train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE)
-            xt = train_ops.gate(xt, train_ops.linear(cs, g) if conds is None else conds[i])
+            gc = train_ops.linear(cs, g) if conds is None else conds[i]
+            # c1 + gate as one launch on the fp16 training path
+            xt = train_ops.conv1d_gate(c1, x, gc, in_slope=LRELU_SLOPE)
+            if xt is None:
+                xt = train_ops.gate(train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE), gc)
             # modules.py:258-259 (xt = c2(xt); x = xt + x): the add in the
             # conv epilogue on the fp16 training path
             x = train_ops.conv1d(c2, xt, residual=x)

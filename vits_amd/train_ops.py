@@ -40,7 +40,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from ._lib import (EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128,
+from ._lib import (EPI_GATE, EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128,
                    TILE_128x256, WDT_BF16, WDT_F16, WDT_F32, ConvWgradDesc, check)
 from .ops import (T256, PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
                   layer_norm_channels, layer_norm_channels_backward, make_desc, make_out,
@@ -171,6 +171,7 @@ def prepacked(net: nn.Module):
     if wdt is not None and _io16(wdt):
         mods = [m for m in net.modules() if supported(m)
                 and any(p.is_cuda for p in m.parameters(recurse=False))]
+    gates = [bool(GATE_FUSED and getattr(m, "_vits_gate", False)) for m in mods]
     if not mods:
         yield
         return
@@ -190,7 +191,8 @@ def prepacked(net: nn.Module):
         e.w, e.cout, e.cin, e.k = w32.data_ptr(), cout, cin, k
         e.img, e.m_pad, e.cin_pad = img.data_ptr(), m_pad, cin_pad
         e.img_t, e.m_pad_t, e.cin_pad_t = img_t.data_ptr(), m_pad_t, cin_pad_t
-        items.append((m, (w, (img, img_t), wdt), w32))
+        e.gate = int(gates[i])  # (the forward image of a fused gate conv: interleaved rows)
+        items.append((m, (w, (img, img_t), wdt, gates[i]), w32))
     check(_lib.load().vits_conv1d_pack16_pairs(arr, len(mods), wdt, _stream_ptr(items[0][2].device)),
           "vits_conv1d_pack16_pairs")
     prev = {m: _PREPACK.get(m) for m, _, _ in items}
@@ -697,7 +699,7 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0,
         y = torch.matmul(w[:, :, 0].to(t16), x.to(t16))
         return y if module.bias is None else y + module.bias.to(t16)[:, None]
     ent = _PREPACK.get(module)
-    pre = ent[1] if (ent is not None and ent[0] is w and ent[2] == wdt) else None
+    pre = ent[1] if (ent is not None and ent[0] is w and ent[2] == wdt and not ent[3]) else None
     return conv1d_hip(x, w, module.bias, module.dilation[0], module.padding[0], in_slope, wdt,
                       residual, pre)
 
@@ -1035,3 +1037,120 @@ class Conv2dRowsHip16(torch.autograd.Function):
                   "vits_conv1d_wgrad_split")
             dw = dwv.view(O, k0, C, k1).permute(0, 2, 1, 3).contiguous()
         return dx, dw, db, None, None, None, None, None, None
+
+
+
+# ---------------------------------------------------------------------------
+# conv -> gate as one launch (WN modules.py:136-146, ResBlock2 modules.py:252-255)
+# ---------------------------------------------------------------------------
+# in_layer / convs1 convs whose output only feeds the tanh * sigmoid gate run
+# the GATE epilogue (gate-interleaved weight rows) and write the
+# pre-activation for the gate's backward in the same launch; VITS_GATE_FUSED=0
+# keeps the separate conv + GateHip16 kernels
+GATE_FUSED = os.environ.get("VITS_GATE_FUSED", "1") != "0"
+
+
+def _pack16_pair_gate(w32, wdtype):
+    """(gate-interleaved forward image, natural input-gradient image) of one
+    weight: vits_conv1d_pack16_pairs with gate = 1."""
+    cout, cin, k = w32.shape
+    dt = _TORCH_16[wdtype]
+    m_pad, cin_pad = (cout + 127) // 128 * 128, (cin + 15) // 16 * 16
+    m_pad_t, cin_pad_t = (cin + 127) // 128 * 128, (cout + 15) // 16 * 16
+    img = torch.empty(cin_pad // 16, k, 2, m_pad, 8, dtype=dt, device=w32.device)
+    img_t = torch.empty(cin_pad_t // 16, k, 2, m_pad_t, 8, dtype=dt, device=w32.device)
+    arr = (_lib.Pack16Layer * 1)()
+    e = arr[0]
+    e.w, e.cout, e.cin, e.k = w32.data_ptr(), cout, cin, k
+    e.img, e.m_pad, e.cin_pad = img.data_ptr(), m_pad, cin_pad
+    e.img_t, e.m_pad_t, e.cin_pad_t = img_t.data_ptr(), m_pad_t, cin_pad_t
+    e.gate = 1
+    check(_lib.load().vits_conv1d_pack16_pairs(arr, 1, wdtype, _stream_ptr(w32.device)),
+          "vits_conv1d_pack16_pairs")
+    return img, img_t
+
+
+class ConvGateHip16(torch.autograd.Function):
+    """acts = tanh(xin[:, :H] + g[:, :H]) * sigmoid(xin[:, H:] + g[:, H:]),
+    xin = conv1d(leaky_relu(x, in_slope), W) + b, as ONE conv launch: the
+    GATE epilogue on gate-interleaved weight rows (fp32 gate arithmetic on
+    the fp32 accumulator) also writes xin (fp16) for the backward.  Backward:
+    the gate backward kernel (dxin, the cond gradient summed over time)
+    then the conv's input / weight gradients (Conv1dHip16's kernels).
+    x, g, acts, xin fp16; W / b fp32 masters."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, g, dilation: int, padding: int, in_slope: float,
+                wdtype: int, pre=None):
+        if x.stride(2) != 1:
+            x = x.contiguous()
+        B, _, T = x.shape
+        w32 = weight.detach().float().contiguous()
+        cout, cin, k = w32.shape
+        H = cout // 2
+        n_out = T + 2 * padding - (k - 1) * dilation
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        img, img_t = pre if pre is not None else _pack16_pair_gate(w32, wdtype)
+        layer, layer_t = _layers16((img, img_t), w32.shape, dilation, padding, wdtype, b32, n_out,
+                                   T)
+        layer.epi = EPI_GATE
+        acts = torch.empty(B, H, n_out, device=x.device, dtype=x.dtype)
+        xin = torch.empty(B, cout, n_out, device=x.device, dtype=x.dtype)
+        cond = None if g is None else g.detach().float().contiguous()
+        d = make_desc(layer, x, make_out(acts), out1=make_out(xin), in_slope=in_slope, tin=T,
+                      n_out=n_out, cond=cond, io16=True)
+        conv1d_launch(d, B, x.device)
+        ctx.layer_t = layer_t
+        ctx.save_for_backward(x, w32, xin, g)
+        ctx.conf = (dilation, padding, in_slope, wdtype, bias is not None)
+        return acts
+
+    @staticmethod
+    def backward(ctx, dacts):
+        x, w32, xin, g = ctx.saved_tensors
+        dil, pad, slope, wdtype, has_bias = ctx.conf
+        B, C2, T = xin.shape
+        H = C2 // 2
+        k = w32.shape[2]
+        dacts = dacts.to(xin.dtype)
+        if dacts.stride(2) != 1:
+            dacts = dacts.contiguous()
+        dxin = torch.empty(B, C2, T, device=xin.device, dtype=xin.dtype)
+        want_dg = g is not None and ctx.needs_input_grad[3]
+        dg = torch.empty(B, C2, device=xin.device, dtype=torch.float32) if want_dg else None
+        g16 = None if g is None else g.to(xin.dtype)
+        if g16 is not None and g16.stride(1) != 1:
+            g16 = g16.contiguous()
+        check(_lib.load().vits_gate_backward_io16(
+            dacts.data_ptr(), dacts.stride(0), dacts.stride(1), xin.data_ptr(), xin.stride(0),
+            xin.stride(1), None if g16 is None else g16.data_ptr(),
+            0 if g16 is None else g16.stride(0), dxin.data_ptr(), dxin.stride(0), dxin.stride(1),
+            None if dg is None else dg.data_ptr(), B, H, T, wdtype, _stream_ptr(xin.device)),
+            "vits_gate_backward_io16")
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _run(dxin, ctx.layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
+                      gmask_slope=slope, io16=True)
+        ctx.layer_t = None
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dw, db = wgrad(dxin, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype,
+                           split=True)
+        return (dx, dw, db, None if dg is None else dg.to(g.dtype), None, None, None, None, None)
+
+
+def conv1d_gate(module: nn.Module, x: torch.Tensor, g, in_slope: float = 1.0):
+    """gate(module(leaky_relu(x, in_slope)), g) (WN / ResBlock2, the conv's
+    output feeding only the gate) as one ConvGateHip16 launch inside a 16-bit
+    autocast region on a ROCm device; None when that does not apply (the
+    caller runs conv1d + gate)."""
+    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+    if (not GATE_FUSED or wdt is None or not _io16(wdt) or not supported(module)
+            or module.out_channels % 2):
+        return None
+    t16 = _TORCH_16[wdt]
+    w = weight_norm_effective(module)
+    ent = _PREPACK.get(module)
+    pre = ent[1] if (ent is not None and ent[0] is w and ent[2] == wdt and ent[3]) else None
+    return ConvGateHip16.apply(x if x.dtype == t16 else x.to(t16), w, module.bias,
+                               None if g is None else g.to(t16), module.dilation[0],
+                               module.padding[0], in_slope, wdt, pre)
