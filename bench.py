@@ -565,6 +565,19 @@ def dry_run_line(args, world, rank, dist):
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"}}
 
 
+def _guarded(name, fn, *a, **k):
+    """fn(*a, **k), or {"error": ...} when it raises (reported in the line)."""
+    try:
+        return fn(*a, **k)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        traceback.print_exc()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        return {"error": f"{name}: {type(e).__name__}: {e}"[:400]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -626,10 +639,13 @@ def main():
     # one rank also C3 = the train_stft step at batch 64 on one GPU
     train = train_c3 = None
     if not args.no_train:
-        train = train_leg(args, device, rank, world, dist, args.train_batch)
+        # a leg that raises (a VitsAmdError shape / support check, deterministic
+        # on every rank) is reported in the line instead of losing the whole
+        # line; a GPU fault still ends the process
+        train = _guarded("train", train_leg, args, device, rank, world, dist, args.train_batch)
         if world == 1 and args.train_batch_c3 and args.train_batch_c3 != args.train_batch:
-            train_c3 = train_leg(args, device, rank, world, dist, args.train_batch_c3,
-                                 cpu_base=False)
+            train_c3 = _guarded("train_c3", train_leg, args, device, rank, world, dist,
+                                args.train_batch_c3, cpu_base=False)
 
     model = build_model(device)
     B, Tx, Ty = args.batch, args.tx, args.ty
@@ -691,8 +707,9 @@ def main():
                     "flops_per_launch": int(per_launch_flops),
                     "conv_ms_per_step": round(s["total_ms"] / args.steps, 3)}
 
-    longform = None if args.no_longform else longform_leg(model, device, rank)
-    kern = None if args.no_kernels else kernels_leg(device)
+    longform = None if args.no_longform else _guarded("longform", longform_leg, model, device,
+                                                      rank)
+    kern = None if args.no_kernels else _guarded("kernels", kernels_leg, device)
     if kern:
         for name, k in kern.items():
             if not isinstance(k, dict):
