@@ -75,8 +75,6 @@ extern "C" {
 #define VITS_TILE_64x256 1
 #define VITS_TILE_32x256 2
 #define VITS_TILE_64x128 3  /* chosen by the library for small grids of 128x128 layers */
-#define VITS_TILE_128x256 4 /* 16-bit operands with weights from global memory: 2x2  */
-                            /* waves of 64x128 (A fragments feed 4 MFMAs, B 2)      */
 
 typedef struct vits_conv_out {
   float* y;               /* output [B][*][y_cstride]                        */
@@ -386,8 +384,9 @@ int vits_attention_forward(const float* q, const float* k, const float* v, float
 /* MFMA arithmetic; mask from lengths (scores.masked_fill(-1e4) of the      */
 /* x_mask outer product); keep [B][H][T][T] uint8 (NULL: no dropout)        */
 /* scales the probabilities by keep * keep_scale as nn.Dropout does.       */
-/* The forward writes lse [B][H][T] (fp32 log-sum-exp per query) for the    */
-/* backward, which recomputes P and writes dq, dk, dv (same layout/dtype);  */
+/* The forward writes lse [B][H][T][2] (fp32 row max m and 1 / row sum per */
+/* query) for the backward, which recomputes P = exp(S - m) / l and writes */
+/* dq, dk, dv (same layout/dtype);                                          */
 /* delta [B][H][T] fp32 is its scratch.  head_dim in {32, 64, 96, 128}.    */
 /* ---------------------------------------------------------------------- */
 int vits_attention_train_forward(const void* q, const void* k, const void* v,

@@ -250,7 +250,13 @@ __global__ __launch_bounds__(64) void attn_train_fwd_kernel(
       const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * lhi;
       ob[(int64_t)d * Tn + qi] = (T)(o[t][r] * inv);
     }
-  if (lhi == 0) lse[((int64_t)b * H + h) * Tn + qi] = m_run + logf(l_run);
+  // (m, 1/l) per query, not m + log(l): a fully masked row has m = -1e4 and
+  // -1e4 + log(l) is not representable closely enough in fp32 (ulp ~1e-3)
+  if (lhi == 0) {
+    const int64_t e = ((int64_t)b * H + h) * Tn + qi;
+    lse[2 * e] = m_run;
+    lse[2 * e + 1] = inv;
+  }
 }
 
 // kernel A: delta and dQ, one wave per (b, h, 32 queries)
@@ -292,7 +298,8 @@ __global__ __launch_bounds__(64) void attn_train_bwd_dq_kernel(
   }
   dl += __shfl_xor(dl, 32, 64);
   if (qvalid && lhi == 0) delta[roff + qi] = dl;
-  const float lq = qvalid ? lse[roff + qi] : 0.f;
+  const float mq = qvalid ? lse[2 * (roff + qi)] : 0.f;
+  const float iq = qvalid ? lse[2 * (roff + qi) + 1] : 0.f;
   f32x16 acc[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t)
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(64) void attn_train_bwd_dq_kernel(
       float ds = 0.f;
       if (key < Tn && qvalid) {
         const bool filled = qmasked || key >= len;
-        const float p = expf((filled ? -1e4f : s[r]) - lq);
+        const float p = expf((filled ? -1e4f : s[r]) - mq) * iq;
         const float m = kp ? (kp[key] ? keep_scale : 0.f) : 1.f;
         ds = filled ? 0.f : p * (dp[r] * m - dl);
       }
@@ -406,7 +413,8 @@ __global__ __launch_bounds__(64) void attn_train_bwd_dkv_kernel(
       float ds = 0.f, pv = 0.f;
       if (qq < Tn && kvalid) {
         const bool filled = qq >= len || ki >= len;
-        const float p = expf((filled ? -1e4f : s[r]) - lse[roff + qq]);
+        const float p = expf((filled ? -1e4f : s[r]) - lse[2 * (roff + qq)]) *
+                        lse[2 * (roff + qq) + 1];
         const float m = keep ? (keep[(roff + qq) * Tn + ki] ? keep_scale : 0.f) : 1.f;
         pv = p * m;
         ds = filled ? 0.f : p * (dp[r] * m - delta[roff + qq]);

@@ -78,7 +78,6 @@ bool ga16(const vits_conv1d_desc* d, int n) {
     const char* e = getenv("VITS_GA16");
     return e ? e[0] - '0' : 1;
   }();
-  if (d[0].tile == VITS_TILE_128x256) return true;  // (only on the global-weight path)
   if (mode == 0) return false;
   if (mode == 2) return true;
   int kmax = 0;

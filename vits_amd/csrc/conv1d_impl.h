@@ -171,7 +171,7 @@ struct ConvGroup {
 // half the bytes of the fp32-I/O kernel; accumulation stays fp32.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false,
           bool GA = false>
-__global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P || BM * BN >= 128 * 256) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
+__global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
   static_assert(!IO16 || WT != VITS_WDT_F32, "IO16 needs a 16-bit operand type");
   const int gi = (int)blockIdx.z / G.batch;
   const vits_conv1d_desc& p = G.d[gi];
@@ -1052,9 +1052,9 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P ||
           rmask = tl < p.y_rowpad || tl >= p.y_rowpad + p.y_rowvalid;
         }
         if (n < p.n_out) {
-          // (in halves of 8 rows on the 128x256 tile: 8 accumulator sub-tiles
-          // are live, so 16-row temporaries would spill)
-          constexpr int RH = TM * TN >= 8 ? 8 : 16;
+          // (row blocks of RH: 8 would halve the temporaries of tiles with 8
+          // live accumulator sub-tiles)
+          constexpr int RH = 16;
 #pragma unroll
           for (int r0 = 0; r0 < 16; r0 += RH) {
           float v[RH];
@@ -1234,10 +1234,8 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
     if (e.tile != d.tile || e.epi != d.epi || (e.split < e.m) != (d.split < d.m) ||
         e.wdtype != d.wdtype)
       return VITS_E_UNSUP;
-    const int bm = (d.tile == VITS_TILE_128x128 || d.tile == VITS_TILE_128x256) ? 128
-                   : d.tile == VITS_TILE_32x256 ? 32 : 64;
-    const int bn = (d.tile == VITS_TILE_64x256 || d.tile == VITS_TILE_32x256 ||
-                    d.tile == VITS_TILE_128x256) ? 256 : 128;
+    const int bm = d.tile == VITS_TILE_128x128 ? 128 : d.tile == VITS_TILE_32x256 ? 32 : 64;
+    const int bn = d.tile == VITS_TILE_64x256 || d.tile == VITS_TILE_32x256 ? 256 : 128;
     blocks += (long)((e.n_out + bn - 1) / bn) * ((e.m + bm - 1) / bm) * g.batch;
   }
   switch (d.tile) {
@@ -1270,13 +1268,6 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
     }
     case VITS_TILE_32x256:
       return launch_tile<32, 256, 1, 4, WT, GA>(g, s);
-    case VITS_TILE_128x256:
-      // 16-bit operands on the global-memory weight path only (a 128-row W
-      // stage in LDS would not fit two buffers): 64x128 per wave, so each A
-      // fragment (global) feeds 4 MFMAs and each B fragment (LDS) 2 - half
-      // the vector-memory bytes per MFMA of the 64x64 wave tiles
-      if constexpr (GA) return launch_tile<128, 256, 2, 2, WT, GA>(g, s);
-      return VITS_E_UNSUP;
     default:
       return VITS_E_UNSUP;
   }

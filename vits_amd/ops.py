@@ -20,8 +20,8 @@ import torch
 from . import _lib
 from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, WDT_F32P, WDT_F32S, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
                    ResblockPairDesc,
-                   EPI_UPSAMPLE, TILE_128x128, TILE_128x256, TILE_32x256, TILE_64x128, TILE_64x256,
-                   TILE_ROWS, check)
+                   EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS,
+                   check)
 
 # ---------------------------------------------------------------------------
 # plumbing
@@ -97,8 +97,6 @@ def _pick_tile_bf16(m: int, k: int) -> int:
     """bf16-MFMA tile (same sweep, BF=1): short kernels on >= 128 rows are
     fastest as 128x128 (k=3: 430 vs 340 TF/s), long ones as 64x256
     (k=11: 730 vs 555), 64-row k<=7 as 64x128, 32 rows as 32x256."""
-    if T256 and m >= 128:
-        return TILE_128x256
     if m <= 32:
         return TILE_32x256
     if k <= 3:
@@ -108,13 +106,7 @@ def _pick_tile_bf16(m: int, k: int) -> int:
     return TILE_64x128
 
 
-TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, TILE_64x128: 128,
-             TILE_128x256: 256}
-# 16-bit layers with >= 128 rows on the 128x256 global-weight tile (A/B switch)
-T256 = os.environ.get("VITS_T256", "0") != "0"
-# K-chunks of global-weight (GA) 16-bit groups sized by the X window only
-# (their weights never enter LDS); 0: the LDS-weight budget too (A/B switch)
-GA_KC = os.environ.get("VITS_GA_KC", "0") != "0"
+TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, TILE_64x128: 128}
 W_TILE_FLOATS = 4096                                   # conv1d.hip VITS_W_TILE
 X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::floats
 
@@ -362,10 +354,9 @@ def io16_kc(layer: PackedConv) -> int:
     bm, bn = TILE_ROWS[layer.tile], TILE_COLS[layer.tile]
     xrs = bn + (layer.k - 1) * layer.dil + 8
     xbudget = 6144 if bn <= 128 else 10240
-    ga = GA_KC or layer.tile == TILE_128x256  # (io16 = 2 groups run the GA path)
     for kc in (64, 48, 32):
         if (kc * layer.k <= LOWP_KCK and layer.cin_pad % kc == 0
-                and (ga or kc * layer.k * bm // 2 <= 6144) and kc * xrs <= xbudget):
+                and kc * layer.k * bm // 2 <= 6144 and kc * xrs <= xbudget):
             return kc
     return 16
 

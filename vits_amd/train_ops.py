@@ -41,8 +41,8 @@ from torch import nn
 
 from . import _lib
 from ._lib import (EPI_GATE, EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128,
-                   TILE_128x256, WDT_BF16, WDT_F16, WDT_F32, ConvWgradDesc, check)
-from .ops import (T256, PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
+                   WDT_BF16, WDT_F16, WDT_F32, ConvWgradDesc, check)
+from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
                   layer_norm_channels, layer_norm_channels_backward, make_desc, make_out,
                   weight_norm_effective)
 
@@ -59,8 +59,6 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
     k7: 307 -> 377 TF/s)."""
     if m > 32 and n_out is not None and n_out <= 128:
         return TILE_128x128 if (m >= 128 and k <= 5) else TILE_64x128
-    if T256 and m >= 128:
-        return TILE_128x256
     if 64 < m <= 128 and 3 < k <= 7:
         return TILE_64x128
     return _pick_tile_bf16(m, k)
@@ -72,10 +70,8 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
 # MFMA k-step per chunk and waits on every chunk's loads.
 TRAIN_KCK = int(os.environ.get("VITS_TRAIN_KCK", "64"))
 _GA_ALL = os.environ.get("VITS_GA16") == "2"  # weights from global memory: no W LDS budget
-_TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32,
-            TILE_128x256: 128}
-_TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256,
-            TILE_128x256: 256}
+_TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32}
+_TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256}
 
 
 def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
@@ -88,7 +84,7 @@ def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
     xbudget = (6144 if bn <= 128 else 10240) if io16 else (3072 if bn <= 128 else 5120)
     for kc in (64, 48, 32):
         if (kc * k <= TRAIN_KCK and cin_pad % kc == 0
-                and (_GA_ALL or tile == TILE_128x256 or kc * k * bm // 2 <= 6144)
+                and (_GA_ALL or kc * k * bm // 2 <= 6144)
                 and kc * xrs <= xbudget):
             return kc
     return 16
@@ -836,8 +832,8 @@ class AttentionHip(torch.autograd.Function):
     """out = dropout(softmax(masked_fill(q k^T / sqrt(D), mask == 0, -1e4))) v
     on [B, H*D, T] channel-major q / k / v (the projection convs' outputs,
     no transposes), mask = the outer product of the length mask, fp32 MFMA
-    (vits_attention_train_forward / _backward: the forward keeps O and the
-    per-query log-sum-exp, the backward recomputes P).  ``keep`` (uint8 [B,
+    (vits_attention_train_forward / _backward: the forward keeps O and each
+    query's softmax max and normaliser, the backward recomputes P).  ``keep`` (uint8 [B,
     H, T, T] or None) is nn.Dropout's keep mask, applied as keep / (1 - p)."""
 
     @staticmethod
@@ -848,7 +844,7 @@ class AttentionHip(torch.autograd.Function):
         code = WDT_F16 if dt == torch.float16 else WDT_F32
         q, k, v = q.contiguous(), k.to(dt).contiguous(), v.to(dt).contiguous()
         out = torch.empty_like(q)
-        lse = torch.empty(B, heads, T, device=q.device, dtype=torch.float32)
+        lse = torch.empty(B, heads, T, 2, device=q.device, dtype=torch.float32)  # (m, 1/l)
         scale = 1.0 / (1.0 - p) if keep is not None else 1.0
         check(_lib.load().vits_attention_train_forward(
             q.data_ptr(), k.data_ptr(), v.data_ptr(), None if keep is None else keep.data_ptr(),
