@@ -924,7 +924,7 @@ def _rows_desc(img, wdtype, rows, chans, k, pad_left, x, x_off, x_cstride, x_bst
                lp, T, in_slope, bias=None, gmask=None, gmask_off=0, gmask_slope=1.0):
     tile = _pick_tile_train(rows, k, n_rows_out * L)
     kc = _train_kc(img.shape[0] * 16, k, 1, tile, True)
-    while x_cgroup % kc:
+    while x_cgroup and x_cgroup % kc:
         kc //= 2
     d = _lib.ConvDesc()
     d.x = x.data_ptr() + x.element_size() * x_off
@@ -979,8 +979,8 @@ class Conv2dRowsHip16(torch.autograd.Function):
         y = torch.zeros(B, O, F_out + 2 * ROW_PAD, L, device=x.device, dtype=x.dtype)
         b32 = None if bias is None else bias.detach().float().contiguous()
         d = _rows_desc(img, wdtype, O, k0 * C, k1, p1, x, ROW_PAD * L, Fp * L, C * Fp * L,
-                       s0 * L, C, L, L, F_out, y, ROW_PAD * L, y.stride(1), y.stride(0), L, lp,
-                       T, in_slope, bias=b32)
+                       s0 * L, C if k0 > 1 else 0, L, L, F_out, y, ROW_PAD * L, y.stride(1),
+                       y.stride(0), L, lp, T, in_slope, bias=b32)
         conv1d_launch(d, B, x.device)
         ctx.save_for_backward(x, w32)
         ctx.conf = (s0, p1, lp, T, in_slope, wdtype, bias is not None, F_out)
@@ -1005,8 +1005,10 @@ class Conv2dRowsHip16(torch.autograd.Function):
                 # [(i', o)][c][j] -> rows c, virtual channels (i', o), taps reversed
                 wp = w32[:, :, taps, :].permute(2, 0, 1, 3).reshape(len(taps) * O, C, k1)
                 img = _pack16_img(wp.contiguous(), True, wdtype)
+                # (one tap: the virtual channels are the plain channels o)
+                cg = O if len(taps) > 1 else 0
                 d = _rows_desc(img, wdtype, C, len(taps) * O, k1, k1 - 1 - p1, dy, ROW_PAD * L,
-                               dy.stride(1), dy.stride(0), L, O, -L, L, Q, dx,
+                               dy.stride(1), dy.stride(0), L, cg, -L, L, Q, dx,
                                (ROW_PAD + rho) * L, dx.stride(1), dx.stride(0), s0 * L, lp, T, 1.0,
                                gmask=x if slope != 1.0 else None,
                                gmask_off=(ROW_PAD + rho) * L, gmask_slope=slope)
@@ -1025,7 +1027,7 @@ class Conv2dRowsHip16(torch.autograd.Function):
             wd.dbias = None if db is None else db.data_ptr()
             wd.wdtype = wdtype
             wd.io16 = 1
-            wd.x_rowlen, wd.x_rowmul, wd.x_cgroup, wd.x_gstride = L, s0 * L, C, L
+            wd.x_rowlen, wd.x_rowmul, wd.x_cgroup, wd.x_gstride = L, s0 * L, C if k0 > 1 else 0, L
             lib = _lib.load()
             nws = int(lib.vits_conv1d_wgrad_workspace(wd, B))
             ws = torch.empty(max(nws, 1), device=x.device, dtype=torch.float32)
