@@ -1003,7 +1003,8 @@ class Conv2dRowsHip16(torch.autograd.Function):
                 if not taps or Q <= 0:
                     continue
                 # [(i', o)][c][j] -> rows c, virtual channels (i', o), taps reversed
-                wp = w32[:, :, taps, :].permute(2, 0, 1, 3).reshape(len(taps) * O, C, k1)
+                # (a slice, not an index list: no host->device copy under capture)
+                wp = w32[:, :, rho::s0, :].permute(2, 0, 1, 3).reshape(len(taps) * O, C, k1)
                 img = _pack16_img(wp.contiguous(), True, wdtype)
                 # (one tap: the virtual channels are the plain channels o)
                 cg = O if len(taps) > 1 else 0
