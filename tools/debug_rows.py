@@ -26,6 +26,7 @@ for sub, (fft, hop) in zip(net.mfd.discriminators, [(128, 32), (256, 64), (512, 
         D.STFT_D_ROWS = False
         b = sub(m)
         D.STFT_D_ROWS = True
+    assert a.shape == b.shape, (a.shape, b.shape)
     err = (a.float() - b.float()).abs().max().item() / b.float().abs().max().item()
     print(f"fft {fft}: out {tuple(a.shape)} vs {tuple(b.shape)} rel err {err:.3e}", flush=True)
     # layer by layer on the torch path's intermediates

@@ -135,7 +135,8 @@ class STFTDiscriminator(nn.Module):
                                                      layer.padding[1], lp, T, slope, wdt)
                 slope = 1.0
             assert hp.shape[1] == 1 and hp.shape[2] == 1 + 2 * R
-            return hp[:, 0, R, lp:lp + T]
+            # [B, 1, T] like the reference's h.squeeze(1).squeeze(2) of [B, 1, 1, T]
+            return hp[:, :, R, lp:lp + T]
         if STFT_D_HIP_ALL and wdt is not None and layers and all(
                 _freq_conv_ok(l) for l in layers if isinstance(l, Conv2d)):
             # every remaining layer on the HIP training conv, the LeakyReLU
