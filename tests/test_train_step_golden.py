@@ -126,10 +126,19 @@ def _batch(G, device):
     return out
 
 
-def _run_step(G, cfg, device, fp16):
+def _run_step(G, cfg, device, fp16, perturb=0.0):
     """One step on the golden inputs; returns (step, outputs, G params
-    before, D params before) with the gradients left on the parameters."""
+    before, D params before) with the gradients left on the parameters.
+    perturb: every parameter element scaled by (1 +- perturb), random signs
+    (seeded), before the step."""
     st = _make_step(cfg, device, fp16)
+    if perturb:
+        gen = torch.Generator().manual_seed(123)
+        with torch.no_grad():
+            for net in (st.net_g, st.net_d):
+                for p in net.parameters():
+                    sgn = torch.randint(0, 2, p.shape, generator=gen).to(p) * 2 - 1
+                    p.mul_(1 + perturb * sgn)
     g0 = {k: p.detach().clone() for k, p in st.net_g.named_parameters()}
     d0 = {k: p.detach().clone() for k, p in st.net_d.named_parameters()}
     with _Replay(G):
@@ -300,20 +309,26 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
     one layer's kernels cannot hide inside an aggregate.  Three runs of the
     same step on the same inputs: HIP fp16 (this repo's training kernels),
     torch fp16 autocast (the reference's own arithmetic: MIOpen fp16 convs,
-    torch gates) and fp32 (torch fp32 convs: the reference's fp32 step).
-    For every parameter whose fp32 gradient exceeds 1e-3 of its network's
-    total norm:
+    torch gates) and torch fp16 autocast again with every parameter scaled
+    by (1 +- 2^-11) (random signs: the size of one fp16 rounding), which
+    measures how far fp16 rounding noise alone moves each gradient.
 
-    * clean parameters (torch16 vs fp32 cosine >= 0.999): the HIP gradient
-      vs torch16's directly, cosine >= 0.99 and norm ratio within 10 %;
-    * every parameter: HIP's error against fp32 no worse than twice
-      torch16's, in angle, 1 - cos(HIP, fp32) <= 2 (1 - cos(t16, fp32)) +
-      0.01, and in norm, |log(|HIP| / |fp32|)| <= 2 |log(|t16| / |fp32|)| +
-      0.05.  On this tiny model the late decoder's fp16 gradients are
-      noise-dominated for BOTH fp16 paths (measured on MI355X: torch16 vs
-      fp32 cosines down to -0.29, HIP's down to 0.22), so a direct HIP-vs-
-      torch16 bar cannot hold there; a wrong kernel still fails the relative
-      bar on every parameter torch16 gets right."""
+    Some gradients of this step are chaotic in fp16: the MR-STFT loss's log
+    magnitudes differentiate as 1 / |X| on near-empty bins of a random-init
+    generator's output, so the late decoder's gradients change direction
+    under the perturbation (measured on MI355X: cosine(torch16,
+    torch16-perturbed) down to ~0.1 for g.dec.conv_pre.weight, and
+    torch16 vs fp32 down to -0.29).  A fixed bar cannot hold there for ANY
+    fp16 implementation, so each parameter gets its own bar from its own
+    noise: for every parameter whose gradient exceeds 1e-3 of its network's
+    total norm,
+
+        1 - cos(HIP, t16)       <= 3 (1 - cos(t16', t16)) + 0.01
+        |log(|HIP| / |t16|)|    <= 3 |log(|t16'| / |t16|)| + 0.05
+
+    i.e. on a parameter fp16 noise does not move (most of them: >= half must
+    have cos(t16', t16) >= 0.999) HIP must match torch16 to cosine 0.99 and
+    norm 5 %; a wrong kernel fails there, on the parameters it feeds."""
     from vits_amd import discriminators, train_ops
 
     G, cfg = _load()
@@ -324,35 +339,25 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
         mp.setattr(discriminators, "STFT_D_HIP", False)
         st, *_ = _run_step(G, cfg, device, True)
         g_t16 = _grads(st)
-    st, *_ = _run_step(G, cfg, device, False)
-    g_f32 = _grads(st)
+        st, *_ = _run_step(G, cfg, device, True, perturb=2.0 ** -11)
+        g_pp = _grads(st)
     del st
-    assert set(g_hip) == set(g_t16) == set(g_f32)
-    hip_t16 = grad_agreement(g_hip, g_t16, g_f32)
-    hip_f32 = grad_agreement(g_hip, g_f32, g_f32)
-    t16_f32 = grad_agreement(g_t16, g_f32, g_f32)
-    bad, clean, worst_clean, worst_rel = [], 0, None, None
-    for k, (cos, ratio) in hip_t16.items():
-        ch, rh = hip_f32[k]
-        ct, rt = t16_f32[k]
-        if ct >= 0.999:
-            clean += 1
-            if worst_clean is None or cos < worst_clean[1]:
-                worst_clean = (k, cos, ratio)
-            if cos < COS_MIN or abs(ratio - 1.0) > NORM_TOL:
-                bad.append(("direct", k, cos, ratio))
-        ang = (1 - ch) - 2 * (1 - ct)
-        nrm = abs(np.log(rh)) - 2 * abs(np.log(rt))
-        if worst_rel is None or ang > worst_rel[1]:
-            worst_rel = (k, ang, ch, ct)
+    assert set(g_hip) == set(g_t16) == set(g_pp)
+    hip_t16 = grad_agreement(g_hip, g_t16, g_t16)
+    pp_t16 = grad_agreement(g_pp, g_t16, g_t16)
+    bad, stable, worst = [], 0, None
+    for k, (ch, rh) in hip_t16.items():
+        cp, rp = pp_t16[k]
+        stable += cp >= 0.999
+        ang = (1 - ch) - 3 * (1 - cp)
+        nrm = abs(np.log(rh)) - 3 * abs(np.log(rp))
+        if worst is None or ang > worst[1]:
+            worst = (k, ang, ch, cp)
         if ang > 0.01 or nrm > 0.05:
-            bad.append(("relative", k, ch, ct, rh, rt))
-    print(f"{len(hip_t16)} parameters compared, {clean} clean; worst clean "
-          f"cos(HIP16, torch16): {worst_clean[0]} cos={worst_clean[1]:.5f} "
-          f"ratio={worst_clean[2]:.4f}; worst relative angle: {worst_rel[0]} "
-          f"cos vs fp32 HIP {worst_rel[2]:.4f} torch16 {worst_rel[3]:.4f}")
-    assert clean >= len(hip_t16) // 2, (clean, len(hip_t16))
+            bad.append((k, ch, cp, rh, rp))
+    print(f"{len(hip_t16)} parameters compared, {stable} stable under the perturbation; "
+          f"worst: {worst[0]} cos(HIP, t16) {worst[2]:.5f} cos(t16', t16) {worst[3]:.5f}")
+    assert stable >= len(hip_t16) // 2, (stable, len(hip_t16))
     assert not bad, bad[:10]
 
 
-COS_MIN, NORM_TOL = 0.99, 0.10

@@ -153,6 +153,9 @@ def _layers16(pre, shape, dil: int, pad_left: int, wdtype: int, bias, n_out: int
 _PREPACK: dict = {}
 
 
+PREPACK = os.environ.get("VITS_PREPACK", "1") != "0"  # A/B switch
+
+
 @contextlib.contextmanager
 def prepacked(net: nn.Module):
     """Inside a 16-bit autocast region on the GPU: pack the 16-bit forward
@@ -164,7 +167,7 @@ def prepacked(net: nn.Module):
     for this scope only (the weights change at the next optimizer step)."""
     wdt = autocast_wdtype("cuda")
     mods = []
-    if wdt is not None and _io16(wdt):
+    if PREPACK and wdt is not None and _io16(wdt):
         mods = [m for m in net.modules() if supported(m)
                 and any(p.is_cuda for p in m.parameters(recurse=False))]
     gates = [bool(GATE_FUSED and getattr(m, "_vits_gate", False)) for m in mods]
@@ -870,6 +873,9 @@ class AttentionHip(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None
 
 
+ATTN_HIP = os.environ.get("VITS_ATTN_HIP", "1") != "0"  # A/B switch
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
               lengths: torch.Tensor | None, p_drop: float, training: bool):
     """MultiHeadAttention.attention's output on the HIP training kernels, or
@@ -877,7 +883,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     in 32/64/96/128, q / k / v not of one length): the caller runs torch."""
     wdt = autocast_wdtype("cuda") if q.device.type == "cuda" else None
     D = q.shape[1] // heads
-    if (wdt is None or lengths is None or D not in (32, 64, 96, 128) or q.shape != k.shape
+    if (not ATTN_HIP or wdt is None or lengths is None or D not in (32, 64, 96, 128) or q.shape != k.shape
             or k.shape != v.shape or q.dtype not in (torch.float16, torch.float32)):
         return None
     keep = None
