@@ -140,16 +140,19 @@ def _errors(G, d, res):
 
 
 @pytest.mark.gpu
-def test_mwsd_gpu_fp16_autocast_vs_reference(device, monkeypatch):
+@pytest.mark.parametrize("rows", [False, True])
+def test_mwsd_gpu_fp16_autocast_vs_reference(device, monkeypatch, rows):
     """fp16 autocast (loss scaled by 1024 before the fp16 backward, as
     GradScaler does) vs the fp32 golden; the bar is the reference's own fp16
     arithmetic on this GPU (torch's autocast convs for every layer), within
     2x (+1e-3).  Measured on MI355X: scores 7e-3 (HIP) vs 1.2e-2 (torch),
     d/dy 6.2e-2 vs 1.0e-1, d/dmag 8.0e-2 vs 6.4e-2, worst parameter
-    gradient norm 1.2e-2 vs 7.0e-3."""
+    gradient norm 1.2e-2 vs 7.0e-3.  rows: the STFT discriminators' layers
+    2+ as row-joined HIP convs (discriminators.STFT_D_ROWS, off by default)."""
     from vits_amd import discriminators, train_ops
 
     G = _load()
+    monkeypatch.setattr(discriminators, "STFT_D_ROWS", rows)
     d = _build(device)
     hip = _errors(G, d, _run(d, G, device, autocast=True, loss_scale=1024.0))
     with monkeypatch.context() as mp:

@@ -522,10 +522,12 @@ def test_attention_train_fwd_bwd_vs_torch(device, dtype, T, D, p):
         assert err <= tol, (what, err)
 
 
-def test_attention_train_dropout_statistics(device):
+def test_attention_train_dropout_statistics(device, monkeypatch):
     """train_ops.attention under autocast: the keep mask is drawn with keep
     probability 1 - p (nn.Dropout's law), and the eval path (training=False)
-    equals the dropout-free kernel."""
+    equals the dropout-free kernel.  (VITS_ATTN_HIP: off by default, see
+    train_ops.ATTN_HIP)"""
+    monkeypatch.setattr(train_ops, "ATTN_HIP", True)
     torch.manual_seed(1)
     B, H, D, T = 4, 2, 64, 96
     q, k, v = (torch.randn(B, H * D, T, device=device).half() for _ in range(3))

@@ -310,25 +310,27 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
     same step on the same inputs: HIP fp16 (this repo's training kernels),
     torch fp16 autocast (the reference's own arithmetic: MIOpen fp16 convs,
     torch gates) and torch fp16 autocast again with every parameter scaled
-    by (1 +- 2^-11) (random signs: the size of one fp16 rounding), which
-    measures how far fp16 rounding noise alone moves each gradient.
+    by (1 +- 2^-11) (random signs: one fp16 rounding), which measures how far
+    fp16 rounding noise alone moves each gradient.
 
-    Some gradients of this step are chaotic in fp16: the MR-STFT loss's log
-    magnitudes differentiate as 1 / |X| on near-empty bins of a random-init
-    generator's output, so the late decoder's gradients change direction
-    under the perturbation (measured on MI355X: cosine(torch16,
-    torch16-perturbed) down to ~0.1 for g.dec.conv_pre.weight, and
-    torch16 vs fp32 down to -0.29).  A fixed bar cannot hold there for ANY
-    fp16 implementation, so each parameter gets its own bar from its own
-    noise: for every parameter whose gradient exceeds 1e-3 of its network's
-    total norm,
+    Part of this step's gradient is chaotic in fp16: the random-init
+    generator's waveform carries fp16 rounding noise at about -66 dB, which
+    dominates its quiet STFT bins, and the MR-STFT loss's log magnitudes
+    differentiate as 1 / |X| there, so the late decoder's gradients follow
+    the rounding noise (measured on MI355X with tools/grad_noise.py: ~280 of
+    ~500 parameters keep cosine >= 0.999 under the perturbation, ~150 fall
+    below 0.9, some to 0.35; the chaotic ones also move between two HIP runs,
+    whose wgrad split-K sums are not ordered).  So:
 
-        1 - cos(HIP, t16)       <= 3 (1 - cos(t16', t16)) + 0.01
-        |log(|HIP| / |t16|)|    <= 3 |log(|t16'| / |t16|)| + 0.05
-
-    i.e. on a parameter fp16 noise does not move (most of them: >= half must
-    have cos(t16', t16) >= 0.999) HIP must match torch16 to cosine 0.99 and
-    norm 5 %; a wrong kernel fails there, on the parameters it feeds."""
+    * every parameter the perturbation leaves in place (cos(t16', t16) >=
+      0.99, at least half of them - all discriminator, encoder and flow
+      layers): cos(HIP, t16) >= 0.99 and |log(|HIP| / |t16|)| <= 0.05 + 3
+      |log(|t16'| / |t16|)|;
+    * the chaotic rest, as a distribution: the median cos(HIP, t16) no lower
+      than the median cos(t16', t16) - 0.1 (a wrong decoder kernel moves the
+      whole distribution, rounding noise moves single parameters).
+    Parameters whose gradient is below 1e-3 of its network's total norm are
+    skipped (grad_agreement)."""
     from vits_amd import discriminators, train_ops
 
     G, cfg = _load()
@@ -345,19 +347,22 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
     assert set(g_hip) == set(g_t16) == set(g_pp)
     hip_t16 = grad_agreement(g_hip, g_t16, g_t16)
     pp_t16 = grad_agreement(g_pp, g_t16, g_t16)
-    bad, stable, worst = [], 0, None
+    bad, stable, ch_c, cp_c = [], 0, [], []
     for k, (ch, rh) in hip_t16.items():
         cp, rp = pp_t16[k]
-        stable += cp >= 0.999
-        ang = (1 - ch) - 3 * (1 - cp)
-        nrm = abs(np.log(rh)) - 3 * abs(np.log(rp))
-        if worst is None or ang > worst[1]:
-            worst = (k, ang, ch, cp)
-        if ang > 0.01 or nrm > 0.05:
-            bad.append((k, ch, cp, rh, rp))
+        if cp >= 0.99:
+            stable += 1
+            if ch < 0.99 or abs(np.log(rh)) > 0.05 + 3 * abs(np.log(rp)):
+                bad.append((k, ch, cp, rh, rp))
+        else:
+            ch_c.append(ch)
+            cp_c.append(cp)
+    med_h = float(np.median(ch_c)) if ch_c else 1.0
+    med_p = float(np.median(cp_c)) if cp_c else 1.0
     print(f"{len(hip_t16)} parameters compared, {stable} stable under the perturbation; "
-          f"worst: {worst[0]} cos(HIP, t16) {worst[2]:.5f} cos(t16', t16) {worst[3]:.5f}")
+          f"chaotic {len(ch_c)}: median cos(HIP, t16) {med_h:.4f}, cos(t16', t16) {med_p:.4f}")
     assert stable >= len(hip_t16) // 2, (stable, len(hip_t16))
     assert not bad, bad[:10]
+    assert med_h >= med_p - 0.1, (med_h, med_p)
 
 

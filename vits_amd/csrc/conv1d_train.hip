@@ -582,26 +582,28 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
 // ---- weight image for the 16-bit forward kernel ------------------------------
 // element i of the image out[c/16][j][(c%16)/8][m][c%8] (rows m / channels c
 // are (co, ci) or, transposed, (ci, co) with the tap order reversed)
+// element i of the image out[c/16][j][(c%16)/8][m][c%8] (rows m / channels c
+// are (co, ci) or, transposed, (ci, co) with the tap order reversed; gate:
+// gate-interleaved rows, row 2q = output q, 2q+1 = cout/2 + q, VITS_EPI_GATE)
 template <typename T>
-__device__ __forceinline__ void pack16_elem(const float* __restrict__ w, int cout, int cin, int k,
-                                            int transpose, T* __restrict__ out, int m_pad,
-                                            int64_t i, int gate = 0) {
-  const int c8 = (int)(i & 7);
-  int64_t r = i >> 3;
-  const int m = (int)(r % m_pad);
-  r /= m_pad;
-  const int half = (int)(r & 1);
-  r >>= 1;
-  const int j = (int)(r % k);
-  const int cg = (int)(r / k);
+__device__ __forceinline__ void pack16_elem32(const float* __restrict__ w, int cout, int cin,
+                                              int k, int transpose, T* __restrict__ out,
+                                              int m_pad, int i, int gate) {
+  const int c8 = i & 7;
+  int r = i >> 3;
+  const int rq = r / m_pad;
+  const int m = r - rq * m_pad;
+  const int half = rq & 1;
+  const int jq = rq >> 1;
+  const int cg = jq / k;
+  const int j = jq - cg * k;
   const int c = cg * 16 + half * 8 + c8;
   float v = 0.f;
   if (!transpose) {
-    // gate-interleaved rows (VITS_EPI_GATE): row 2q = output q, 2q+1 = cout/2 + q
     const int src = gate ? ((m & 1) ? (cout >> 1) + (m >> 1) : (m >> 1)) : m;
-    if (m < cout && c < cin) v = w[((int64_t)src * cin + c) * k + j];
+    if (m < cout && c < cin) v = w[(src * cin + c) * k + j];
   } else {
-    if (m < cin && c < cout) v = w[((int64_t)c * cin + m) * k + (k - 1 - j)];
+    if (m < cin && c < cout) v = w[(c * cin + m) * k + (k - 1 - j)];
   }
   out[i] = (T)v;
 }
@@ -611,43 +613,38 @@ __device__ __forceinline__ void pack16_elem(const float* __restrict__ w, int cou
 // too, one graph node instead of two per conv
 template <typename T>
 __global__ void pack16_pair_kernel(const float* __restrict__ w, int cout, int cin, int k,
-                                   T* __restrict__ out, int m_pad, int64_t total,
-                                   T* __restrict__ out_t, int m_pad_t, int64_t total_t) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total + total_t;
-       i += (int64_t)gridDim.x * blockDim.x) {
+                                   T* __restrict__ out, int m_pad, int total,
+                                   T* __restrict__ out_t, int m_pad_t, int total_t) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total + total_t;
+       i += gridDim.x * blockDim.x) {
     if (i < total)
-      pack16_elem<T>(w, cout, cin, k, 0, out, m_pad, i);
+      pack16_elem32<T>(w, cout, cin, k, 0, out, m_pad, i, 0);
     else
-      pack16_elem<T>(w, cout, cin, k, 1, out_t, m_pad_t, i - total);
+      pack16_elem32<T>(w, cout, cin, k, 1, out_t, m_pad_t, i - total, 0);
   }
 }
 
 // both images of up to PACK_LIST layers per launch (vits_conv1d_pack16_pairs):
-// the flat index runs over the layers' concatenated images, start[] holds
-// each layer's first element
+// blockIdx.y = layer, blockIdx.x strides over that layer's two images (32-bit
+// index math: one image is < 2^31 elements, checked on the host)
 constexpr int PACK_LIST = 48;
 struct PackList {
   vits_pack16_layer l[PACK_LIST];
-  int64_t start[PACK_LIST + 1];
   int n;
 };
 
 template <typename T>
 __global__ __launch_bounds__(256) void pack16_pairs_kernel(const PackList L) {
-  const int64_t end = L.start[L.n];
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < end;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int q = 0;
-    while (q + 1 < L.n && L.start[q + 1] <= i) ++q;  // (layers in order; <= 48)
-    const vits_pack16_layer& e = L.l[q];
-    const int64_t total = (int64_t)e.cin_pad * e.k * e.m_pad;
-    const int64_t r = i - L.start[q];
-    if (r < total)
-      pack16_elem<T>(e.w, e.cout, e.cin, e.k, 0, reinterpret_cast<T*>(e.img), e.m_pad, r,
-                     e.gate);
+  const vits_pack16_layer& e = L.l[blockIdx.y];
+  const int total = e.cin_pad * e.k * e.m_pad;
+  const int end = total + e.cin_pad_t * e.k * e.m_pad_t;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < end; i += gridDim.x * 256) {
+    if (i < total)
+      pack16_elem32<T>(e.w, e.cout, e.cin, e.k, 0, reinterpret_cast<T*>(e.img), e.m_pad, i,
+                       e.gate);
     else
-      pack16_elem<T>(e.w, e.cout, e.cin, e.k, 1, reinterpret_cast<T*>(e.img_t), e.m_pad_t,
-                     r - total);
+      pack16_elem32<T>(e.w, e.cout, e.cin, e.k, 1, reinterpret_cast<T*>(e.img_t), e.m_pad_t,
+                       i - total, 0);
   }
 }
 
@@ -658,28 +655,9 @@ __global__ void pack16_kernel(const float* __restrict__ w, int cout, int cin, in
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < zero_n;
        i += (int64_t)gridDim.x * blockDim.x)
     zero[i] = 0.f;
-  // out[c/16][j][(c%16)/8][m][c%8]; rows m / channels c are (co, ci) or,
-  // transposed, (ci, co) with the tap order reversed
-  const int64_t total = (int64_t)cin_pad * k * m_pad;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i & 7);
-    int64_t r = i >> 3;
-    const int m = (int)(r % m_pad);
-    r /= m_pad;
-    const int half = (int)(r & 1);
-    r >>= 1;
-    const int j = (int)(r % k);
-    const int cg = (int)(r / k);
-    const int c = cg * 16 + half * 8 + c8;
-    float v = 0.f;
-    if (!transpose) {
-      if (m < cout && c < cin) v = w[((int64_t)m * cin + c) * k + j];
-    } else {
-      if (m < cin && c < cout) v = w[((int64_t)c * cin + m) * k + (k - 1 - j)];
-    }
-    out[i] = (T)v;
-  }
+  const int total = cin_pad * k * m_pad;  // (< 2^31, checked on the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
+    pack16_elem32<T>(w, cout, cin, k, transpose, out, m_pad, i, 0);
 }
 
 }  // namespace
@@ -756,17 +734,18 @@ extern "C" int vits_conv1d_pack16_pair(const float* w, int cout, int cin, int k,
                    cin_pad_t >= cout);
   const int64_t total = (int64_t)cin_pad * k * m_pad;
   const int64_t total_t = (int64_t)cin_pad_t * k * m_pad_t;
-  const int64_t nblk = (total + total_t + 255) / 256;
+  VITS_CHECK_SHAPE(total + total_t < ((int64_t)1 << 31));  // (32-bit index math)
+  const int64_t nblk = (total + total_t + 2047) / 2048;
   const int blocks = (int)(nblk < 8192 ? nblk : 8192);
   hipStream_t s = as_stream(stream);
   if (wdtype == VITS_WDT_F16)
     hipLaunchKernelGGL(pack16_pair_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, w, cout, cin,
-                       k, reinterpret_cast<_Float16*>(out), m_pad, total,
-                       reinterpret_cast<_Float16*>(out_t), m_pad_t, total_t);
+                       k, reinterpret_cast<_Float16*>(out), m_pad, (int)total,
+                       reinterpret_cast<_Float16*>(out_t), m_pad_t, (int)total_t);
   else if (wdtype == VITS_WDT_BF16)
     hipLaunchKernelGGL(pack16_pair_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, w, cout, cin, k,
-                       reinterpret_cast<__bf16*>(out), m_pad, total,
-                       reinterpret_cast<__bf16*>(out_t), m_pad_t, total_t);
+                       reinterpret_cast<__bf16*>(out), m_pad, (int)total,
+                       reinterpret_cast<__bf16*>(out_t), m_pad_t, (int)total_t);
   else
     return VITS_E_ARG;
   return vits_launch_status();
@@ -781,6 +760,7 @@ extern "C" int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int 
   const int chans = transpose ? cout : cin;
   VITS_CHECK_SHAPE(m_pad % 128 == 0 && m_pad >= rows && cin_pad % 16 == 0 && cin_pad >= chans);
   const int64_t total = (int64_t)cin_pad * k * m_pad;
+  VITS_CHECK_SHAPE(total < ((int64_t)1 << 31));  // (32-bit index math)
   const int64_t most = total > zero_n ? total : zero_n;
   const int64_t nblk = (most + 255) / 256;
   const int blocks = (int)(nblk < 4096 ? nblk : 4096);
@@ -804,7 +784,7 @@ extern "C" int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, 
   for (int b0 = 0; b0 < n; b0 += PACK_LIST) {
     PackList L;
     L.n = n - b0 < PACK_LIST ? n - b0 : PACK_LIST;
-    L.start[0] = 0;
+    int64_t most = 0;
     for (int q = 0; q < L.n; ++q) {
       const vits_pack16_layer& e = layers[b0 + q];
       VITS_CHECK_ARG(e.w && e.img && e.img_t && e.cout > 0 && e.cin > 0 && e.k > 0);
@@ -813,16 +793,20 @@ extern "C" int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, 
                        e.cin_pad >= e.cin);
       VITS_CHECK_SHAPE(e.m_pad_t % 128 == 0 && e.m_pad_t >= e.cin && e.cin_pad_t % 16 == 0 &&
                        e.cin_pad_t >= e.cout);
+      const int64_t both = (int64_t)e.cin_pad * e.k * e.m_pad +
+                           (int64_t)e.cin_pad_t * e.k * e.m_pad_t;
+      VITS_CHECK_SHAPE(both < ((int64_t)1 << 31) &&
+                       (int64_t)e.cout * e.cin * e.k < ((int64_t)1 << 31));
       L.l[q] = e;
-      L.start[q + 1] = L.start[q] + (int64_t)e.cin_pad * e.k * e.m_pad +
-                       (int64_t)e.cin_pad_t * e.k * e.m_pad_t;
+      if (both > most) most = both;
     }
-    const int64_t nblk = (L.start[L.n] + 255) / 256;
-    const int blocks = (int)(nblk < 8192 ? nblk : 8192);
+    // ~8 elements per thread for the largest layer, at most 1024 blocks each
+    const int64_t bx = (most + 2047) / 2048;
+    const dim3 grid((unsigned)(bx < 1024 ? (bx < 1 ? 1 : bx) : 1024), (unsigned)L.n);
     if (wdtype == VITS_WDT_F16)
-      hipLaunchKernelGGL(pack16_pairs_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, L);
+      hipLaunchKernelGGL(pack16_pairs_kernel<_Float16>, grid, dim3(256), 0, s, L);
     else
-      hipLaunchKernelGGL(pack16_pairs_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, L);
+      hipLaunchKernelGGL(pack16_pairs_kernel<__bf16>, grid, dim3(256), 0, s, L);
     const int rc = vits_launch_status();
     if (rc) return rc;
   }

@@ -166,8 +166,10 @@ class STFTDiscriminator(nn.Module):
 
 
 STFT_D_HIP = True  # test switch: False keeps every STFT-discriminator conv on torch
-# layers 2+ as row-joined HIP convs on the row-padded layout (train_ops.Conv2dRowsHip16)
-STFT_D_ROWS = os.environ.get("VITS_STFT_D_ROWS", "1") != "0"
+# layers 2+ as row-joined HIP convs on the row-padded layout (train_ops.Conv2dRowsHip16):
+# off by default - measured 82.3 vs 80.1 ms per B=32 step against MIOpen's
+# NHWC fp16 kernels (the 64-row tiles and the padded rows: see DESIGN 4f)
+STFT_D_ROWS = os.environ.get("VITS_STFT_D_ROWS", "0") != "0"
 
 
 def _rows_ok(layers) -> bool:

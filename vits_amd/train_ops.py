@@ -873,7 +873,11 @@ class AttentionHip(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None
 
 
-ATTN_HIP = os.environ.get("VITS_ATTN_HIP", "1") != "0"  # A/B switch
+# the HIP training attention (AttentionHip) in MultiHeadAttention: off by
+# default - measured 82.3 vs 80.5 ms per B=32 step against torch's
+# batched-GEMM attention (fp32 32x32x2 MFMAs, one wave per 32 queries: 256
+# single-wave workgroups at T=100 leave the chip latency-bound)
+ATTN_HIP = os.environ.get("VITS_ATTN_HIP", "0") != "0"
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
