@@ -688,15 +688,20 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
       // (sched_barrier): left alone, the scheduler sinks the global A loads
       // into the middle of the MFMA block and the next block then waits on
       // them (measured: ~12 MFMAs of cover instead of 24)
+      // (each half first waits for its own B fragments - issued a whole
+      // MFMA block earlier - so the waitcnt pass does not put an
+      // lgkmcnt(0) after the next step's B reads, which left them no cover)
       for (; st + 2 <= nst; st += 2) {
         next();
         loadA(s0 + st + 1, a1);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         loadB(buf, j, g, bh1, bm1, bl1);
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, bh0, bm0, bl0);
         __builtin_amdgcn_sched_barrier(0);
         next();
         loadA(s0 + st + 2, a0);  // (st + 2 == nst: the next chunk's first step)
+        __builtin_amdgcn_s_waitcnt(0xc07f);
         if (st + 2 < nst) loadB(buf, j, g, bh0, bm0, bl0);
         __builtin_amdgcn_sched_barrier(0);
         mma(a1, bh1, bm1, bl1);
@@ -859,27 +864,37 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
       }
       if (st < nsteps) mma(a0, bh0, bm0, bl0);
     } else if constexpr (BF) {
-      // k-step = (tap j, 16 channels): A = one 16-byte bf16x8 read per
-      // 32-row fragment (W image [j][c8][row][8]); B = 8 channel rows of the
-      // fp32 X window at column n + j*dil, rounded to bf16 in registers
-      const char* wbytes = reinterpret_cast<const char*>(ws);
-      const int c8n = kc >> 3;
+      // k-step = (tap j, 16 channels): A = one 16-byte read per 32-row
+      // fragment of the W image [j][c8][row][8], B = 8 channels of the
+      // [t][kcp] window at column n + j*dil.  A of step st = (j, group g),
+      // g fastest, sits at image row j * c8n + 2 g + lhi = 2 st + lhi
+      // (c8n = 2 G): linear in st.  B's window offset j * dil * kcp + 16 g
+      // is advanced incrementally (no division by G in the loop), and the
+      // loads of step st + 1 are pinned ahead of step st's MFMAs
+      // (sched_barrier), as on the GA path
+      const char* wlane = reinterpret_cast<const char*>(ws) +
+                          ((int64_t)(lhi * BM + wm + l32) << 4);
+      const lp_t* xlane = reinterpret_cast<const lp_t*>(xs) + (wn + l32 + xsh) * kcp + 8 * lhi;
       const int G = kc >> 4;       // 16-channel groups per tap
-      const int nsteps = k * G;    // k-steps of this chunk, (j, g) with g fastest
+      const int nsteps = k * G;    // k-steps of this chunk
+      const int jstep = dil * kcp - 16 * (G - 1);
+      int boff = 0, g = 0;         // B offset / group of the next load
       auto load = [&](int st, lpx8* a, lpx8* bb) {
-        const int j = st / G;
-        const int g = st - j * G;
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
-          a[mi] = *reinterpret_cast<const lpx8*>(
-              wbytes + ((int64_t)((j * c8n + 2 * g + lhi) * BM + wm + mi * 32 + l32) << 4));
+          a[mi] = *reinterpret_cast<const lpx8*>(wlane + ((int64_t)(2 * st * BM + mi * 32) << 4));
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
-          const lp_t* xp = reinterpret_cast<const lp_t*>(xs) +
-                           (wn + ni * 32 + l32 + j * dil + xsh) * kcp + 16 * g + 8 * lhi;
+          const lp_t* xp = xlane + boff + ni * 32 * kcp;
           const lpx4 lo = *reinterpret_cast<const lpx4*>(xp);
           const lpx4 hi = *reinterpret_cast<const lpx4*>(xp + 4);
           bb[ni] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        if (++g == G) {
+          g = 0;
+          boff += jstep;
+        } else {
+          boff += 16;
         }
       };
       auto mma = [&](const lpx8* a, const lpx8* bb) {
@@ -896,13 +911,28 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
       // MFMAs of step s (the read past the last step stays inside the
       // stage's padded LDS and is never consumed)
       lpx8 a0[TM], b0[TN], a1[TM], b1[TN];
+      // no scalar load may be pending when the loop starts: SMEM returns out
+      // of order with LDS, and the waitcnt pass would then wait for ALL LDS
+      // reads (lgkmcnt(0)) at each step's first MFMA instead of leaving the
+      // next step's TM + TN reads in flight
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt / expcnt untouched
       load(0, a0, b0);
       int st = 0;
+      // each step first waits for its own fragments (issued a whole MFMA
+      // block earlier, so normally landed), then issues the next step's
+      // reads, then its MFMAs: left to itself the waitcnt pass put an
+      // lgkmcnt(0) AFTER the next step's reads, i.e. no LDS latency cover
       for (; st + 2 <= nsteps; st += 2) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         load(st + 1, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
         mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
         load(st + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
         mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
       }
       if (st < nsteps) mma(a0, b0);
     } else {
