@@ -620,51 +620,6 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
     };
     av_t a0[NPL][TM], a1[NPL][TM];
     av_t bh0[TN], bm0[NB], bl0[NB], bh1[TN], bm1[NB], bl1[NB];
-#ifdef VITS_A2
-    // (A/B build) A fragments two k-steps ahead: a third register set, the
-    // sets rotated by moves after each step
-    av_t a2[NPL][TM];
-    loadA(0, a0);
-    loadA(1, a1);
-    gload(0);
-    lstore(xbuf1, 0);
-    __syncthreads();
-    for (int ch = 0; ch < nchunks; ++ch) {
-      const bool more = ch + 1 < nchunks;
-      if (more) gload((ch + 1) * kc);
-      const int buf = ch & 1;
-      const int s0 = ch * nst;
-      int j = 0, g = 0;
-      loadB(buf, 0, 0, bh0, bm0, bl0);
-      for (int st = 0; st < nst; ++st) {
-        loadA(s0 + st + 2, a2);
-        if (++j == k) {
-          j = 0;
-          ++g;
-        }
-        if (st + 1 < nst) loadB(buf, j, g, bh1, bm1, bl1);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(a0, bh0, bm0, bl0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < NPL; ++q)
-#pragma unroll
-          for (int mi = 0; mi < TM; ++mi) {
-            a0[q][mi] = a1[q][mi];
-            a1[q][mi] = a2[q][mi];
-          }
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni) bh0[ni] = bh1[ni];
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni) {
-          bm0[ni] = bm1[ni];
-          bl0[ni] = bl1[ni];
-        }
-      }
-      if (more) lstore(buf ? xbuf1 : xbuf2, (ch + 1) * kc);
-      __syncthreads();
-    }
-#else
     loadA(0, a0);
     gload(0);
     lstore(xbuf1, 0);
@@ -719,7 +674,6 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
       if (more) lstore(buf ? xbuf1 : xbuf2, (ch + 1) * kc);
       __syncthreads();
     }
-#endif
   } else {
 
   if constexpr (WPS)

@@ -32,6 +32,7 @@ torch conv, i.e. the reference's own fp32 arithmetic.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import os
 
@@ -90,10 +91,25 @@ def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
     return 16
 
 
+# per-call weight packs by call site (tools/pack_census.py; VITS_PACK_TRACE=1)
+PACK_TRACE = collections.Counter() if os.environ.get("VITS_PACK_TRACE") == "1" else None
+
+
+def _trace_pack(kind, shape):
+    if PACK_TRACE is not None:
+        import traceback
+
+        fr = [f for f in traceback.extract_stack(limit=8)[:-2]
+              if not f.filename.endswith(("train_ops.py", "function.py"))]
+        site = fr[-1] if fr else traceback.extract_stack(limit=3)[0]
+        PACK_TRACE[(kind, tuple(shape), f"{os.path.basename(site.filename)}:{site.lineno}")] += 1
+
+
 def _pack16(w32: torch.Tensor, transpose: bool, dil: int, pad_left: int, wdtype: int,
             bias: torch.Tensor | None = None, zero: torch.Tensor | None = None,
             n_out: int | None = None, io16: bool = False) -> PackedConv:
     """16-bit weight image (and, in the same launch, clear ``zero``)."""
+    _trace_pack("pack16", w32.shape)
     cout, cin, k = w32.shape
     rows, chans = (cin, cout) if transpose else (cout, cin)
     m_pad = (rows + 127) // 128 * 128
@@ -114,6 +130,7 @@ def _pack16_pair(w32: torch.Tensor, dil: int, pad_left: int, wdtype: int,
     """The forward image and the input-gradient (transposed, tap-reversed)
     image of one weight in ONE launch: (forward PackedConv, backward
     PackedConv)."""
+    _trace_pack("pair", w32.shape)
     cout, cin, k = w32.shape
     dt = _TORCH_16[wdtype]
     m_pad, cin_pad = (cout + 127) // 128 * 128, (cin + 15) // 16 * 16
