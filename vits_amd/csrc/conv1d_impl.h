@@ -643,20 +643,15 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
       // (sched_barrier): left alone, the scheduler sinks the global A loads
       // into the middle of the MFMA block and the next block then waits on
       // them (measured: ~12 MFMAs of cover instead of 24)
-      // (each half first waits for its own B fragments - issued a whole
-      // MFMA block earlier - so the waitcnt pass does not put an
-      // lgkmcnt(0) after the next step's B reads, which left them no cover)
       for (; st + 2 <= nst; st += 2) {
         next();
         loadA(s0 + st + 1, a1);
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         loadB(buf, j, g, bh1, bm1, bl1);
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, bh0, bm0, bl0);
         __builtin_amdgcn_sched_barrier(0);
         next();
         loadA(s0 + st + 2, a0);  // (st + 2 == nst: the next chunk's first step)
-        __builtin_amdgcn_s_waitcnt(0xc07f);
         if (st + 2 < nst) loadB(buf, j, g, bh0, bm0, bl0);
         __builtin_amdgcn_sched_barrier(0);
         mma(a1, bh1, bm1, bl1);
