@@ -555,6 +555,15 @@ typedef struct vits_resblock_pair_desc {
 } vits_resblock_pair_desc;
 int vits_resblock_pair_forward(const vits_resblock_pair_desc* d, int n, int batch, void* stream);
 int vits_resblock_pair_kc(int channels, int k, int dil, int* kc1, int* kc2);
+/* The same pair for 16-bit models (csrc/resblock16.hip; modules.py:250-  */
+/* 260 of a model.half() / bf16 Generator): wdtype VITS_WDT_BF16 / F16;   */
+/* x and y are [B][C][T] tensors of that type (the float pointers of the  */
+/* descriptor reinterpreted), w1 / w2 the 16-bit images                   */
+/* [cin_pad/16][k][2][m_pad][8] of vits_conv1d_desc (w1's rows gate-      */
+/* interleaved); kc1 / kc2 are ignored.  C = 32 or 64, odd k,             */
+/* (k - 1) * dil <= 96, T % 4 == 0.                                       */
+int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch, int wdtype,
+                                 void* stream);
 
 /* Fused RAdam step (radam.py:35-99, the D optimizer of train_stft.py:97) */
 /* over a list of fp32 tensors, one launch per VITS_RADAM_MAX tensors.     */

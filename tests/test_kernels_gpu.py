@@ -530,6 +530,78 @@ def test_resblock_pair_fused(device, C, k, dil, T):
     _close(acc, (refs[0] + refs[1] + refs[2]) / 3, what="mean")
 
 
+@pytest.mark.parametrize("C,k,dil,T", [
+    (32, 3, 1, 12), (32, 11, 5, 300), (64, 7, 3, 2052), (64, 3, 5, 48), (32, 7, 1, 9216),
+    (64, 11, 5, 1000), (64, 11, 1, 500),
+])
+@pytest.mark.parametrize("wdt", [ops.WDT_BF16, ops.WDT_F16])
+def test_resblock_pair16_fused(device, C, k, dil, T, wdt):
+    """csrc/resblock16.hip (the pair of a 16-bit model: 16-bit x / y and
+    weight images, fp32 accumulation, the gated tensor rounded to 16 bits in
+    LDS as the two-conv path rounds it in HBM) against the pair in fp64 on
+    the same 16-bit-rounded inputs and weights: tiles shorter than the
+    sequence, ends inside a tile, the three-branch grouped launch and the
+    branch-mean epilogue.  Tolerance: 2 roundings of the operand type
+    (bf16 2e-2, fp16 3e-3 of the output magnitude)."""
+    dt = {ops.WDT_BF16: torch.bfloat16, ops.WDT_F16: torch.float16}[wdt]
+    tol = 2e-2 if wdt == ops.WDT_BF16 else 3e-3
+    g = torch.Generator().manual_seed(C + k + dil + T + wdt)
+    B = 2
+    packs, refs, xs = [], [], []
+    for j in range(3):
+        x = (torch.randn(B, C, T, generator=g) * 0.5).to(dt)
+        w1 = (torch.randn(C, C, k, generator=g) / (C * k) ** 0.5).to(dt).float()
+        b1 = torch.randn(C, generator=g) * 0.1
+        w2 = (torch.randn(C, C // 2, k, generator=g) / (C * k / 2) ** 0.5).to(dt).float()
+        b2 = torch.randn(C, generator=g) * 0.1
+        cond = torch.randn(B, C, generator=g) * 0.3
+        with ops.pack_lowp(wdt):
+            c1 = ops.pack_conv(w1.to(device), b1.to(device), dilation=dil, gate=True)
+            c2 = ops.pack_conv(w2.to(device), b2.to(device))
+        xd = x.to(device)
+        assert ops.resblock_pair16_supported(c1, c2, xd)
+        packs.append((c1, c2, cond.to(device)))
+        refs.append(_resblock_pair_ref(x.float(), w1, b1, cond, w2, b2, k, dil))
+        xs.append(xd)
+    ys = [torch.full((B, C, T), float("nan"), device=device, dtype=dt) for _ in range(3)]
+    ops.resblock_pair16_launch(tuple(
+        ops.resblock_pair16_desc(c1, c2, xs[j], ys[j], cond=cd)
+        for j, (c1, c2, cd) in enumerate(packs)), B, device, wdt)
+    torch.cuda.synchronize()
+    for j in range(3):
+        _close(ys[j], refs[j], tol=tol, what=f"pair {j}")
+    acc = torch.empty(B, C, T, device=device, dtype=dt)
+    for j, (c1, c2, cd) in enumerate(packs):
+        ops.resblock_pair16_launch(ops.resblock_pair16_desc(
+            c1, c2, xs[j], acc, cond=cd, accumulate=j > 0, post_div=3.0 if j == 2 else 1.0),
+            B, device, wdt)
+    torch.cuda.synchronize()
+    _close(acc, (refs[0] + refs[1] + refs[2]) / 3, tol=2 * tol, what="mean")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_generator16_fused_pairs_match_two_conv_path(device, monkeypatch, dt):
+    """A 16-bit model's Generator with resblock16 pairs on its 32/64-channel
+    stages against its two-conv path (VITS_FUSED_PAIRS16=0): the same
+    rounding points (16-bit gated tensor, one rounding of each output), only
+    the fp32 accumulation order differs - 1e-2 (bf16) / 2e-3 (fp16) of the
+    waveform magnitude."""
+    from common import base_model
+
+    m = base_model(device).to(dt)
+    g = torch.Generator().manual_seed(5)
+    z = (torch.randn(2, 192, 40, generator=g) * 0.7).to(device).to(dt)
+    gg = (torch.randn(2, 1024, generator=g) * 0.5).to(device).to(dt)
+    tol = 1e-2 if dt == torch.bfloat16 else 2e-3
+    with torch.no_grad():
+        monkeypatch.setattr(ops, "FUSED_PAIRS16", True)
+        m.dec.__dict__.pop("_vits_amd_plan", None)
+        a = m.dec(z, gg)
+        monkeypatch.setattr(ops, "FUSED_PAIRS16", False)
+        b = m.dec(z, gg)
+    _close(a, b, tol=tol, what="fused16 vs two-conv")
+
+
 def test_generator_fused_pairs_match_two_conv_path(device, monkeypatch):
     """The Generator with fused pairs on its 32/64-channel stages equals the
     two-conv path (VITS_FUSED_PAIRS=0) to fp32 rounding."""

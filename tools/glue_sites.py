@@ -32,10 +32,24 @@ class Count(TorchDispatchMode):
         name = func.__name__.split(".")[0]
         if name in GLUE and any(isinstance(a, torch.Tensor) and a.is_cuda for a in args):
             site = "?"
-            for f in reversed(traceback.extract_stack(limit=30)):
-                if HERE in f.filename and "glue_sites" not in f.filename:
-                    site = f"{os.path.basename(f.filename)}:{f.lineno} {f.name}"
-                    break
+            node = torch._C._current_autograd_node()
+            if node is not None:
+                # backward: the forward op's site from anomaly mode's traceback
+                tb = node.metadata.get("traceback_", [])
+                lines = "".join(tb).splitlines() if tb else []
+                for ln in reversed(lines):
+                    if HERE in ln and 'File "' in ln:
+                        f = ln.split('File "')[1]
+                        site = "bwd " + os.path.basename(f.split('"')[0]) + ":" + \
+                            f.split("line ")[1].split(",")[0] + " " + type(node).__name__
+                        break
+                else:
+                    site = "bwd ? " + type(node).__name__
+            else:
+                for f in reversed(traceback.extract_stack(limit=30)):
+                    if HERE in f.filename and "glue_sites" not in f.filename:
+                        site = f"{os.path.basename(f.filename)}:{f.lineno} {f.name}"
+                        break
             self.c[(name, site)] += 1
         return func(*args, **(kwargs or {}))
 
@@ -50,7 +64,7 @@ st.step(batch)
 torch.cuda.synchronize()
 torch.autograd.set_multithreading_enabled(False)
 m = Count()
-with m:
+with torch.autograd.detect_anomaly(check_nan=False), m:
     st.step(batch)
 torch.cuda.synchronize()
 tot = sum(m.c.values())

@@ -1,0 +1,335 @@
+// resblock16.hip — one ResBlock2 dilation pair of a 16-bit (bf16 / fp16)
+// Generator as ONE kernel, 16-bit MFMAs (v_mfma_f32_32x32x16_{bf16,f16}),
+// fp32 accumulation, 16-bit activations in HBM:
+//
+//   y = x + c2( tanh(a + sa) * sigmoid(b + sb) ) ,   (a | b) = c1(lrelu(x, slope))
+//
+// (modules.py:250-260: c1 = Conv1d(C, C, k, dil d), c2 = Conv1d(C/2, C, k),
+// sa / sb = the utterance's cond Linear; models.py:306-318 averages the
+// branches: the last pair of each branch accumulates into the stage output).
+//
+// The two-conv path writes the gated tensor to HBM and reads it back, plus
+// the residual: for the 32- / 64-channel stages of a long-form utterance
+// (T = 240,000 / 480,000 samples) that traffic and the two launches' short K
+// loops (K = C * k and C/2 * k) dominate.  Here one workgroup owns a time
+// tile of BN = NG - (k - 1) outputs and all C channels:
+//   staging: the whole c1 input window (C channels x NG + (k-1) dil columns,
+//            lrelu applied, zero outside [0, T)) goes to LDS once, as
+//            [t][C + 8] 16-bit rows (one 16-byte B fragment per lane: 8
+//            channels of one column), 4 channels x 4 steps per unit, the
+//            transpose done in registers (conv1d_impl.h's T4 staging);
+//   phase 1: the c1 GEMM over NG columns (the tile plus c2's (k-1)/2 halo
+//            each side), A fragments (gate-interleaved rows) from the packed
+//            16-bit image in global memory / L2, one k-step ahead; the gate
+//            epilogue writes G[t][C/2 + 8] (16-bit, zero outside [0, L):
+//            c2's own zero padding at the utterance ends);
+//   phase 2: the c2 GEMM straight from G (tap j = column shift j), residual
+//            (x re-read: L2-resident) + bias (+ running branch mean) epilogue
+//            to HBM.
+// Halo columns are recomputed by the neighbouring tile, never exchanged.
+// Every launch holds up to 3 independent pairs (the branches of a stage).
+// Weight images: vits_conv1d_desc's 16-bit layout [cin_pad/16][k][2][m_pad][8]
+// (ops.to_lowp), c1's rows gate-interleaved (row 2q = a_q, 2q+1 = b_q).
+#include <type_traits>
+
+#include "common.h"
+
+namespace {
+
+constexpr int R16_GROUP = 3;
+constexpr int R16_NG = 256;  // phase-1 columns per tile (4 waves x 64)
+struct R16Group {
+  vits_resblock_pair_desc d[R16_GROUP];
+  int n;
+  int batch;
+};
+
+__device__ __forceinline__ float r16_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float r16_tanh(float x) {
+  return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
+}
+
+// LDS geometry (host and device agree): window columns (4-aligned), row
+// pitches in elements, bytes of the whole workgroup
+__host__ __device__ inline int r16_xcols(int k, int dil) {
+  // NG + (k-1) dil window columns + up to 3 of alignment shift, 4-blocks
+  return ((R16_NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
+}
+__host__ __device__ inline int r16_lds_bytes(int C, int k, int dil) {
+  const int xp = C + 8, gp = C / 2 + 8;
+  return 2 * (r16_xcols(k, dil) * xp + (R16_NG + 16) * gp) + 4 * 2 * C + 64;
+}
+
+template <int C, typename T>
+__global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
+  constexpr int H = C / 2;
+  constexpr int TM = C / 32;       // 32-row MFMA tiles of c1 / c2 (one wave row)
+  constexpr int TN = 2;            // 4 waves x 64 columns
+  constexpr int XP = C + 8;        // window row pitch (16-bit elements)
+  constexpr int GP = H + 8;        // gated row pitch
+  constexpr int S1 = C / 16;       // 16-channel slabs of c1's K
+  constexpr int S2 = H / 16;       // ... of c2's K
+  typedef T t8 __attribute__((ext_vector_type(8)));
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  static_assert(C == 32 || C == 64, "32- / 64-channel stages");
+
+  const int gi = (int)blockIdx.z / G.batch;
+  const vits_resblock_pair_desc& p = G.d[gi];
+  const int b = (int)blockIdx.z - gi * G.batch;
+  const int k = p.k;
+  const int dil = p.dil;
+  const int Tn = p.t_len;
+  const int L = p.lengths ? min(Tn, (int)p.lengths[b]) : Tn;
+  const int p1 = (k - 1) * dil / 2;
+  const int p2 = (k - 1) / 2;
+  const int BN = R16_NG - 2 * p2;
+  const int n0 = blockIdx.x * BN;
+  if (n0 >= Tn) return;
+  if (p.lengths && p.len_skip > 0 && n0 >= L + p.len_skip) return;
+
+  extern __shared__ float smem[];
+  float* const erow = smem;                                   // [2C] row constants
+  T* const xs = reinterpret_cast<T*>(smem + 2 * C + 16);      // [xcols][XP]
+  const int xcols = r16_xcols(k, dil);
+  T* const gs = xs + xcols * XP;                              // [NG + 16][GP]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wn = (tid >> 6) * 64;
+  const int l32 = lane & 31;
+  const int lhi = lane >> 5;
+
+  // row constants: c1 bias + cond (gate-interleaved order), c2 bias
+  const float* cond = p.cond ? p.cond + (int64_t)b * p.cond_bstride : nullptr;
+  for (int r = tid; r < 2 * C; r += 256) {
+    float e = 0.f;
+    if (r < C) {
+      const int idx = (r & 1) ? H + (r >> 1) : (r >> 1);
+      if (p.b1) e = p.b1[idx];
+      if (cond) e += cond[idx];
+    } else if (p.b2) {
+      e = p.b2[r - C];
+    }
+    erow[r] = e;
+  }
+
+  // ---- the c1 window -> LDS (lrelu, zero padding), 4 ch x 4 steps per unit
+  const T* xb = reinterpret_cast<const T*>(p.x) + (int64_t)b * p.x_bstride;
+  const int tw0 = n0 - p2 - p1;          // time of window column 0 (before the shift)
+  const int xstart = tw0 & ~3;           // 8-byte aligned block start
+  const int xsh = tw0 - xstart;          // window column c sits at LDS column c + xsh
+  const int nb = xcols >> 2;             // 4-step blocks
+  const float slope = p.in_slope;
+  {
+    const int nunits = (C / 4) * nb;
+    for (int u = tid; u < nunits; u += 256) {
+      const int cq = u % (C / 4);        // channel quad (fastest: distinct LDS banks)
+      const int tb = u / (C / 4);
+      const int tt = xstart + 4 * tb;
+      const bool ok = tt >= 0 && tt < Tn;  // T % 4 == 0: a block is all in or all out
+      t4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (ok) {
+          v[i] = *reinterpret_cast<const t4*>(xb + (int64_t)(4 * cq + i) * p.x_cstride + tt);
+        } else {
+          v[i] = t4{};
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        t4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float f = (float)v[i][e];
+          f = f < 0.f ? f * slope : f;
+          w[i] = (T)f;
+        }
+        *reinterpret_cast<t4*>(xs + (4 * tb + e) * XP + 4 * cq) = w;
+      }
+    }
+  }
+  __syncthreads();
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto mfma = [&](const t8& a, const t8& bb, f32x16 c) -> f32x16 {
+    if constexpr (std::is_same<T, _Float16>::value)
+      return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bb, c, 0, 0, 0);
+    else
+      return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, c, 0, 0, 0);
+  };
+
+  // one GEMM: steps s = slab * k + j (the image's order), A of step s from
+  // the packed image (16 bytes per lane and 32-row fragment, one step
+  // ahead), B from LDS: 8 channels (16 s + 8 lhi ..) of column
+  // col0 + ni * 32 + j * jstride
+  auto gemm = [&](const T* wimg, int m_pad, int nsteps, const T* bsrc, int pitch, int col0,
+                  int jstride) {
+    const T* wl = wimg + ((int64_t)lhi * m_pad + l32) * 8;
+    const int64_t wstep = (int64_t)16 * m_pad;
+    const T* bl = bsrc + (col0 + l32) * pitch + 8 * lhi;
+    auto loadA = [&](int s, t8* a) {
+      const T* w = wl + (int64_t)(s < nsteps ? s : nsteps - 1) * wstep;
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) a[mi] = *reinterpret_cast<const t8*>(w + mi * 32 * 8);
+    };
+    int g = 0, j = 0;
+    auto loadB = [&](t8* bb) {
+      const T* x = bl + j * jstride * pitch + 16 * g;
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) bb[ni] = *reinterpret_cast<const t8*>(x + ni * 32 * pitch);
+      if (++j == k) {
+        j = 0;
+        ++g;
+      }
+    };
+    auto mma = [&](const t8* a, const t8* bb) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma(a[mi], bb[ni], acc[mi][ni]);
+    };
+    t8 a0[TM], b0[TN], a1[TM], b1[TN];
+    loadA(0, a0);
+    loadB(b0);
+    int s = 0;
+    for (; s + 2 <= nsteps; s += 2) {
+      loadA(s + 1, a1);
+      loadB(b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      loadA(s + 2, a0);
+      if (s + 2 < nsteps) loadB(b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (s < nsteps) mma(a0, b0);
+  };
+
+  // ---------------- phase 1: c1 over NG columns from n0 - p2 ---------------
+  gemm(reinterpret_cast<const T*>(p.w1), p.m_pad1, S1 * k, xs, XP, wn + xsh, dil);
+
+  // gate epilogue -> G (zero outside [0, L)); the 16 columns past NG that
+  // phase 2's discarded columns read are zeroed too
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int col = wn + ni * 32 + l32;
+      const int t = n0 - p2 + col;
+      const bool in = t >= 0 && t < L;
+#pragma unroll
+      for (int r = 0; r < 16; r += 4) {
+        // rows rloc, rloc + 1 (a_q, b_q) and rloc + 2, rloc + 3 (a_q+1, b_q+1)
+        const int row = mi * 32 + 4 * lhi + 8 * (r >> 2);
+        const float g0 = r16_tanh(acc[mi][ni][r] + erow[row]) *
+                         r16_sigmoid(acc[mi][ni][r + 1] + erow[row + 1]);
+        const float g1 = r16_tanh(acc[mi][ni][r + 2] + erow[row + 2]) *
+                         r16_sigmoid(acc[mi][ni][r + 3] + erow[row + 3]);
+        typedef T t2 __attribute__((ext_vector_type(2)));
+        t2 v;
+        v[0] = (T)(in ? g0 : 0.f);
+        v[1] = (T)(in ? g1 : 0.f);
+        *reinterpret_cast<t2*>(gs + col * GP + (row >> 1)) = v;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+    }
+  }
+  for (int i = tid; i < 16 * H; i += 256) gs[(R16_NG + i / H) * GP + i % H] = (T)0.f;
+  __syncthreads();
+
+  // ---------------- phase 2: c2 from G --------------------------------------
+  gemm(reinterpret_cast<const T*>(p.w2), p.m_pad2, S2 * k, gs, GP, wn, 1);
+
+  // residual (+ running branch mean) epilogue, 16-bit out
+  T* yb = reinterpret_cast<T*>(p.y) + (int64_t)b * p.y_bstride;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int col = wn + ni * 32 + l32;
+      const int t = n0 + col;
+      if (col < BN && t < Tn) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+          float v = (float)xb[(int64_t)row * p.x_cstride + t] + (acc[mi][ni][r] + erow[C + row]);
+          const int64_t di = (int64_t)row * p.y_cstride + t;
+          if (p.accumulate) v = (float)yb[di] + v;
+          if (p.post_div != 1.0f) v = v / p.post_div;
+          yb[di] = (T)(t < L ? v : 0.f);
+        }
+      }
+    }
+  }
+}
+
+template <int C, typename T>
+int r16_launch(const R16Group& g, hipStream_t s) {
+  int lds = 0, gx = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const vits_resblock_pair_desc& d = g.d[i];
+    const int l = r16_lds_bytes(C, d.k, d.dil);
+    if (l > lds) lds = l;
+    const int BN = R16_NG - (d.k - 1);
+    const int x = (d.t_len + BN - 1) / BN;
+    if (x > gx) gx = x;
+  }
+  if (lds > 160 * 1024) return VITS_E_UNSUP;
+  hipLaunchKernelGGL((resblock16_kernel<C, T>), dim3(gx, 1, g.n * g.batch), dim3(256), lds, s, g);
+  return vits_launch_status();
+}
+
+int r16_check(const vits_resblock_pair_desc& d) {
+  VITS_CHECK_ARG(d.x && d.w1 && d.w2 && d.y);
+  // other workgroups still read x (halos, residual): never write in place
+  VITS_CHECK_ARG(reinterpret_cast<const void*>(d.y) != reinterpret_cast<const void*>(d.x));
+  VITS_CHECK_SHAPE(d.channels == 32 || d.channels == 64);
+  VITS_CHECK_SHAPE(d.k >= 1 && d.k <= 15 && (d.k & 1) == 1 && d.dil >= 1 && d.t_len > 0);
+  VITS_CHECK_SHAPE((d.k - 1) * d.dil <= 96);  // window within the LDS budget
+  // images: [cin_pad/16][k][2][m_pad][8], rows = C (c1 gate-interleaved / c2)
+  VITS_CHECK_SHAPE(d.m_pad1 >= d.channels && d.m_pad2 >= d.channels && (d.m_pad1 & 3) == 0 &&
+                   (d.m_pad2 & 3) == 0);
+  VITS_CHECK_SHAPE(d.cin_pad1 >= d.channels && d.cin_pad2 >= d.channels / 2);
+  // 8-byte x staging: time-contiguous rows, T % 4 == 0, aligned
+  VITS_CHECK_SHAPE((d.t_len & 3) == 0 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
+                   d.x_cstride >= d.t_len && d.y_cstride >= d.t_len &&
+                   (reinterpret_cast<uintptr_t>(d.x) & 7) == 0);
+  VITS_CHECK_SHAPE((reinterpret_cast<uintptr_t>(d.w1) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(d.w2) & 15) == 0);
+  return VITS_OK;
+}
+
+}  // namespace
+
+extern "C" int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch,
+                                            int wdtype, void* stream) {
+  if (!d || n < 1 || n > R16_GROUP || batch < 1) return VITS_E_ARG;
+  if (wdtype != VITS_WDT_BF16 && wdtype != VITS_WDT_F16) return VITS_E_ARG;
+  R16Group g;
+  g.n = n;
+  g.batch = batch;
+  for (int i = 0; i < n; ++i) {
+    const int rc = r16_check(d[i]);
+    if (rc) return rc;
+    if (d[i].channels != d[0].channels) return VITS_E_SHAPE;
+    g.d[i] = d[i];
+  }
+  hipStream_t s = as_stream(stream);
+  const bool f16 = wdtype == VITS_WDT_F16;
+  if (d[0].channels == 32)
+    return f16 ? r16_launch<32, _Float16>(g, s) : r16_launch<32, __bf16>(g, s);
+  return f16 ? r16_launch<64, _Float16>(g, s) : r16_launch<64, __bf16>(g, s);
+}

@@ -228,8 +228,24 @@ class GeneratorPlan:
             raise NotImplementedError("ResBlock2 branches with different dilation counts")
         C, T = xu.shape[1], xu.shape[2]
         io16 = 2 if xu.dtype != torch.float32 else 0  # (2: inference decoder, conv1d.hip ga16)
-        fused = [[_FUSED_PAIRS and not io16 and ops.resblock_pair_supported(pr[0], pr[1], T)
-                  for pr in pairs] for pairs in blocks]
+
+        def can_fuse(pr):
+            if io16:  # 16-bit model, 16-bit activations: csrc/resblock16.hip
+                return ops.resblock_pair16_supported(pr[0], pr[1], xu)
+            return _FUSED_PAIRS and ops.resblock_pair_supported(pr[0], pr[1], T)
+
+        fused = [[can_fuse(pr) for pr in pairs] for pairs in blocks]
+
+        def pair_desc(j, p, dst, **kw):
+            fn = ops.resblock_pair16_desc if io16 else ops.resblock_pair_desc
+            return fn(blocks[j][p][0], blocks[j][p][1], cur[j], dst, cond=cond,
+                      cond_offset=blocks[j][p][2], lengths=lengths, **kw)
+
+        def pair_launch(descs):
+            if io16:
+                ops.resblock_pair16_launch(descs, B, dev, blocks[0][0][0].wdtype)
+            else:
+                ops.resblock_pair_launch(descs, B, dev)
         tmp = [[torch.empty_like(xs), torch.empty_like(xs)] for _ in range(nk)]
         gbuf = [None if all(fused[j]) else
                 torch.empty(B, C // 2, T, device=dev, dtype=xu.dtype) for j in range(nk)]
@@ -248,11 +264,7 @@ class GeneratorPlan:
             if p < npairs - 1:
                 dst = [tmp[j][p & 1] for j in range(nk)]
                 if fj:
-                    ops.resblock_pair_launch(tuple(
-                        ops.resblock_pair_desc(blocks[j][p][0], blocks[j][p][1], cur[j], dst[j],
-                                               cond=cond, cond_offset=blocks[j][p][2],
-                                               lengths=lengths)
-                        for j in fj), B, dev)
+                    pair_launch(tuple(pair_desc(j, p, dst[j]) for j in fj))
                 if cj:
                     descs = grouped(c1_desc(j, p) for j in cj)
                     descs += grouped(make_desc(blocks[j][p][1], gbuf[j],
@@ -269,9 +281,7 @@ class GeneratorPlan:
             for j in range(nk):
                 kw = dict(accumulate=j > 0, post_div=float(nk) if j == nk - 1 else 1.0)
                 if fused[j][p]:
-                    ops.resblock_pair_launch(ops.resblock_pair_desc(
-                        blocks[j][p][0], blocks[j][p][1], cur[j], xs, cond=cond,
-                        cond_offset=blocks[j][p][2], lengths=lengths, **kw), B, dev)
+                    pair_launch(pair_desc(j, p, xs, **kw))
                 else:
                     ops.conv1d_launch_seq([make_desc(blocks[j][p][1], gbuf[j],
                                                      make_out(xs, res=cur[j], **kw),

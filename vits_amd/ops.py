@@ -574,17 +574,22 @@ class ConvTimer:
         self.shapes.append("conv " + "+".join(
             f"m{d.m}c{d.cin}k{d.k}d{d.dil}T{d.n_out}e{d.epi}t{d.tile}" for d in group))
 
-    def launch_pairs(self, lib, group, batch, device):
+    def launch_pairs(self, lib, group, batch, device, wdtype=None):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         stream = torch.cuda.current_stream(device)
         s.record(stream)
         arr = (ResblockPairDesc * len(group))(*group)
-        check(lib.vits_resblock_pair_forward(arr, len(group), batch, stream.cuda_stream),
-              "vits_resblock_pair_forward")
+        if wdtype is None:
+            check(lib.vits_resblock_pair_forward(arr, len(group), batch, stream.cuda_stream),
+                  "vits_resblock_pair_forward")
+        else:
+            check(lib.vits_resblock_pair16_forward(arr, len(group), batch, int(wdtype),
+                                                   stream.cuda_stream),
+                  "vits_resblock_pair16_forward")
         e.record(stream)
         self.records.append((s, e, sum(resblock_pair_flops(d, batch) for d in group)))
-        self.peaks.append(MFMA_PEAK_TFLOPS[WDT_F32])
+        self.peaks.append(MFMA_PEAK_TFLOPS[WDT_F32 if wdtype is None else wdtype])
         self.shapes.append("pair " + "+".join(
             f"C{d.channels}k{d.k}d{d.dil}T{d.t_len}" for d in group))
 
@@ -664,6 +669,59 @@ def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch
     d.lengths = _ptr(lengths)
     d.len_skip = LEN_SKIP.margin if lengths is not None else 0
     return d
+
+
+# fused pairs of 16-bit models (csrc/resblock16.hip): VITS_FUSED_PAIRS16=0
+# keeps their two-conv path
+FUSED_PAIRS16 = os.environ.get("VITS_FUSED_PAIRS16", "1") != "0"
+
+
+def resblock_pair16_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -> bool:
+    """Pairs of a 16-bit model with 16-bit activations that run fused
+    (csrc/resblock16.hip): the 32- and 64-channel stages, any odd k with
+    (k - 1) * dil <= 96, 8-byte aligned time rows (T % 4 == 0)."""
+    C_ = c2.out_channels
+    return (FUSED_PAIRS16 and c1.wdtype in (WDT_BF16, WDT_F16) and c2.wdtype == c1.wdtype
+            and x.dtype == _WDT_TORCH[c1.wdtype] and C_ in (32, 64) and c1.m == C_
+            and c1.cin == C_ and c2.cin == C_ // 2 and c2.m == C_ and c1.k == c2.k
+            and c1.k % 2 == 1 and (c1.k - 1) * c1.dil <= 96 and c2.dil == 1
+            and c1.epi == EPI_GATE and x.shape[2] % 4 == 0 and x.stride(2) == 1
+            and x.stride(1) % 4 == 0 and x.stride(0) % 4 == 0)
+
+
+def resblock_pair16_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch.Tensor, *,
+                         cond: Optional[torch.Tensor] = None, cond_offset: int = 0,
+                         in_slope: float = 0.1, accumulate: bool = False, post_div: float = 1.0,
+                         lengths: Optional[torch.Tensor] = None) -> ResblockPairDesc:
+    """resblock_pair_desc for resblock16 (16-bit x / y, 16-bit images)."""
+    assert x.dtype == y.dtype == _WDT_TORCH[c1.wdtype] and x.stride(2) == 1 and y.stride(2) == 1
+    C_, T = x.shape[1], x.shape[2]
+    d = ResblockPairDesc()
+    d.x, d.x_bstride, d.x_cstride, d.t_len = x.data_ptr(), x.stride(0), x.stride(1), T
+    d.channels, d.in_slope = C_, in_slope
+    d.w1, d.m_pad1, d.cin_pad1, d.kc1 = c1.w.data_ptr(), c1.m_pad, c1.cin_pad, 16
+    d.k, d.dil, d.kc2 = c1.k, c1.dil, 16
+    d.b1 = _ptr(c1.bias)
+    if cond is not None:
+        d.cond, d.cond_bstride = cond.data_ptr() + 4 * cond_offset, cond.stride(0)
+    d.w2, d.m_pad2, d.cin_pad2 = c2.w.data_ptr(), c2.m_pad, c2.cin_pad
+    d.b2 = _ptr(c2.bias)
+    d.y, d.y_bstride, d.y_cstride = y.data_ptr(), y.stride(0), y.stride(1)
+    d.accumulate, d.post_div = int(accumulate), float(post_div)
+    d.lengths = _ptr(lengths)
+    d.len_skip = LEN_SKIP.margin if lengths is not None else 0
+    return d
+
+
+def resblock_pair16_launch(descs, batch: int, device: torch.device, wdtype: int):
+    """One launch of up to 3 independent 16-bit pairs (tuple) or one pair."""
+    group = tuple(descs) if isinstance(descs, (tuple, list)) else (descs,)
+    lib = _lib.load()
+    if ConvTimer.active is not None:
+        return ConvTimer.active.launch_pairs(lib, group, batch, device, wdtype)
+    arr = (ResblockPairDesc * len(group))(*group)
+    check(lib.vits_resblock_pair16_forward(arr, len(group), batch, int(wdtype),
+                                           _stream_ptr(device)), "vits_resblock_pair16_forward")
 
 
 def resblock_pair_flops(d: ResblockPairDesc, batch: int) -> int:
