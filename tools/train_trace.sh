@@ -4,6 +4,10 @@ TAG=${1:-s8}
 OUT=gpurun_out/tt_$TAG
 export TMPDIR=/tmp
 mkdir -p $OUT
+# one unprofiled run first: MIOpen's find step (its kernels, a first-run-only
+# cost kept in the user db) must not land in the R=1 run only - the diff would
+# then drop the STFT discriminators' MIOpen convs as "negative"
+timeout -k 10 300 python3 tools/train_pmc.py --batch 32 --replays 1 > $OUT/warm.log 2>&1 || exit 1
 for R in 1 3; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/r$R -o run -- \
     python3 tools/train_pmc.py --batch 32 --replays $R > $OUT/r$R.log 2>&1 || exit 1
