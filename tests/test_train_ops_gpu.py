@@ -630,3 +630,33 @@ def test_conv_gate_fused_matches_conv_then_gate(device, cin, H, k, dil, T, slope
     for i, (u, v) in enumerate(zip(a, b)):
         err = (u.float() - v.float()).abs().max().item() / u.float().abs().max().item()
         assert err <= 2e-3, (i, err)
+
+
+def test_qkv_cat_matches_three_convs(device, monkeypatch):
+    """Self-attention's q / k / v projections as one HIP conv over the
+    concatenated weight rows (train_ops.conv1d_cat) against three conv1d
+    calls under fp16 autocast: outputs and the gradients of x and of every
+    projection weight / bias agree to 2e-3 of each tensor's max (the input
+    gradient is one K = 3C GEMM instead of three GEMMs and two fp16 adds)."""
+    from vits_amd import attentions
+
+    torch.manual_seed(7)
+    mha = attentions.MultiHeadAttention(192, 192, 2, p_dropout=0.0).to(device)
+    x = torch.randn(4, 192, 100, device=device)
+    gy = torch.randn(4, 192, 100, device=device)
+    mask = torch.ones(4, 1, 100, 100, device=device)
+
+    def run(cat):
+        monkeypatch.setattr(attentions, "QKV_CAT", cat)
+        for p in mha.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.float16):
+            y = mha(xi, xi, mask)
+        y.float().backward(gy)
+        return [y.float(), xi.grad] + [p.grad for p in mha.parameters()]
+
+    a, b = run(False), run(True)
+    for i, (u, v) in enumerate(zip(a, b)):
+        err = (u.float() - v.float()).abs().max().item() / u.float().abs().max().item()
+        assert err <= 2e-3, (i, err)

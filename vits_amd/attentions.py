@@ -7,6 +7,7 @@ flash-style attention kernel, channel LayerNorm) via ``vits_amd.engine``.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import nn
@@ -14,6 +15,11 @@ from torch.nn import functional as F
 
 from . import train_ops
 from .modules import LayerNorm
+
+
+# self-attention's q / k / v projections as one HIP conv under autocast
+# (train_ops.conv1d_cat); VITS_QKV_CAT=0 keeps three
+QKV_CAT = os.environ.get("VITS_QKV_CAT", "1") != "0"
 
 
 class MultiHeadAttention(nn.Module):
@@ -44,7 +50,12 @@ class MultiHeadAttention(nn.Module):
         (train_ops.AttentionHip: MFMA forward + backward, dropout fused)."""
         # 1x1 projections on the HIP training conv under autocast (torch otherwise)
         conv = train_ops.conv1d
-        q, k, v = conv(self.conv_q, x), conv(self.conv_k, c), conv(self.conv_v, c)
+        qkv = (train_ops.conv1d_cat((self.conv_q, self.conv_k, self.conv_v), x)
+               if c is x and QKV_CAT else None)
+        if qkv is not None:  # self-attention: q, k, v as one conv launch
+            q, k, v = qkv
+        else:
+            q, k, v = conv(self.conv_q, x), conv(self.conv_k, c), conv(self.conv_v, c)
         y = train_ops.attention(q, k, v, self.n_heads, lengths, self.p_dropout, self.training)
         if y is None:
             y = self.attention(q, k, v, mask=attn_mask)[0]

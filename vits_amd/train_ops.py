@@ -720,6 +720,27 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0,
                       residual, pre)
 
 
+def conv1d_cat(modules, x: torch.Tensor):
+    """[m(x) for m in modules] for convs of one input and one geometry (the
+    self-attention q / k / v projections, attentions.py:85-87) as ONE HIP
+    conv over their concatenated weight rows: one forward, one input-
+    gradient conv (the three gradients' sum comes out of a single K = 3C
+    GEMM - no adds) and one weight gradient instead of three each.  Returns
+    the outputs as channel slices of one [B, sum(C_out), T] tensor, or None
+    where conv1d would not run the modules on the HIP kernels."""
+    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+    m0 = modules[0]
+    if (wdt is None or not _io16(wdt) or not all(supported(m) for m in modules)
+            or any(m.kernel_size != m0.kernel_size or m.dilation != m0.dilation
+                   or m.padding != m0.padding or m.in_channels != m0.in_channels
+                   or (m.bias is None) != (m0.bias is None) for m in modules)):
+        return None
+    w = torch.cat([weight_norm_effective(m) for m in modules], 0)
+    b = None if m0.bias is None else torch.cat([m.bias for m in modules], 0)
+    y = conv1d_hip(x, w, b, m0.dilation[0], m0.padding[0], 1.0, wdt)
+    return y.split([m.out_channels for m in modules], 1)
+
+
 # 1x1 training convs with T <= this run as hipBLASLt GEMMs (0: always the HIP conv)
 GEMM_1X1_MAX_T = int(os.environ.get("VITS_TRAIN_GEMM1X1", "0"))
 
