@@ -273,7 +273,11 @@ class Generator(nn.Module):
             return None
         ws = [train_ops.module_weight(m) for m in mods]
         y = F.linear(g, torch.cat(ws, 0), torch.cat([m.bias for m in mods]))
-        parts = torch.split(y, [w.shape[0] for w in ws], dim=1)
+        sizes = [w.shape[0] for w in ws]
+        parts = torch.split(y, sizes, dim=1)
+        y32 = train_ops.cond_f32(y)  # one cast for every pair's fused gate
+        if y32 is not None:
+            parts = list(zip(parts, torch.split(y32, sizes, dim=1)))
         k = len(self.resblocks[0].conds)
         return [parts[i * k:(i + 1) * k] for i in range(len(self.resblocks))]
 

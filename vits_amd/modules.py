@@ -77,15 +77,21 @@ class WN(nn.Module):
     def forward(self, x, x_mask, g=None, **kwargs):
         H = self.hidden_channels
         output = None  # zeros_like(x), materialised on first use
+        g32 = None
         if self.gin_channels != 0:
             g = train_ops.linear(self.cond_layer, g)
+            g32 = train_ops.cond_f32(g)  # one cast for every layer's fused gate
         x16 = None  # x rounded to the conv dtype by the fused update (WNUpdate16)
         for i in range(self.n_layers):
             xi = x if x16 is None else x16
             H2 = 2 * H
             g_l = g[:, i * H2:(i + 1) * H2] if self.gin_channels else None
             # in_layer conv + gate as one launch on the fp16 training path
-            acts = train_ops.conv1d_gate(self.in_layers[i], xi, g_l)
+            if g32 is not None:
+                acts = train_ops.conv1d_gate(self.in_layers[i], xi, g32[:, i * H2:(i + 1) * H2],
+                                             g16=g_l)
+            else:
+                acts = train_ops.conv1d_gate(self.in_layers[i], xi, g_l)
             if acts is None:
                 acts = self._gate(train_ops.conv1d(self.in_layers[i], xi),
                                   g if self.gin_channels else None, i)
@@ -141,8 +147,14 @@ class ResBlock2(nn.Module):
             return resblock_infer(self, x, g)
         for i, (c1, c2, cs) in enumerate(zip(self.convs1, self.convs2, self.conds)):
             gc = train_ops.linear(cs, g) if conds is None else conds[i]
+            gc32 = None
+            if isinstance(gc, tuple):  # (16-bit cond, its fp32 copy): Generator._resblock_conds
+                gc, gc32 = gc
             # c1 + gate as one launch on the fp16 training path
-            xt = train_ops.conv1d_gate(c1, x, gc, in_slope=LRELU_SLOPE)
+            if gc32 is not None:
+                xt = train_ops.conv1d_gate(c1, x, gc32, in_slope=LRELU_SLOPE, g16=gc)
+            else:
+                xt = train_ops.conv1d_gate(c1, x, gc, in_slope=LRELU_SLOPE)
             if xt is None:
                 xt = train_ops.gate(train_ops.conv1d(c1, x, in_slope=LRELU_SLOPE), gc)
             # modules.py:258-259 (xt = c2(xt); x = xt + x): the add in the

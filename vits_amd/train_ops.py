@@ -1128,7 +1128,11 @@ class ConvGateHip16(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, g, dilation: int, padding: int, in_slope: float,
-                wdtype: int, pre=None):
+                wdtype: int, pre=None, g16=None):
+        """g: the cond (fp32 or 16-bit, [B, C2(, 1)], channel stride 1); g16
+        (optional, not differentiated): the same values in the operand type
+        for the backward's gate kernel - WN / ResBlock2 cast their whole
+        cond tensor once instead of every layer's slice twice."""
         if x.stride(2) != 1:
             x = x.contiguous()
         B, _, T = x.shape
@@ -1143,12 +1147,18 @@ class ConvGateHip16(torch.autograd.Function):
         layer.epi = EPI_GATE
         acts = torch.empty(B, H, n_out, device=x.device, dtype=x.dtype)
         xin = torch.empty(B, cout, n_out, device=x.device, dtype=x.dtype)
-        cond = None if g is None else g.detach().float().contiguous()
+        cond = None
+        if g is not None:
+            cond = g.detach()
+            if cond.dtype != torch.float32 or cond.stride(1) != 1:
+                cond = cond.float().contiguous()
         d = make_desc(layer, x, make_out(acts), out1=make_out(xin), in_slope=in_slope, tin=T,
                       n_out=n_out, cond=cond, io16=True)
         conv1d_launch(d, B, x.device)
         ctx.layer_t = layer_t
-        ctx.save_for_backward(x, w32, xin, g)
+        ctx.g_dtype = None if g is None else g.dtype
+        ctx.g_shape = None if g is None else tuple(g.shape)
+        ctx.save_for_backward(x, w32, xin, g16 if g16 is not None else g)
         ctx.conf = (dilation, padding, in_slope, wdtype, bias is not None)
         return acts
 
@@ -1165,7 +1175,7 @@ class ConvGateHip16(torch.autograd.Function):
         dxin = torch.empty(B, C2, T, device=xin.device, dtype=xin.dtype)
         want_dg = g is not None and ctx.needs_input_grad[3]
         dg = torch.empty(B, C2, device=xin.device, dtype=torch.float32) if want_dg else None
-        g16 = None if g is None else g.to(xin.dtype)
+        g16 = None if g is None else g.to(xin.dtype)  # (a no-op when g16 was given)
         if g16 is not None and g16.stride(1) != 1:
             g16 = g16.contiguous()
         check(_lib.load().vits_gate_backward_io16(
@@ -1182,10 +1192,24 @@ class ConvGateHip16(torch.autograd.Function):
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
             dw, db = wgrad(dxin, x, k, dil, pad, slope, with_bias=has_bias, wdtype=wdtype,
                            split=True)
-        return (dx, dw, db, None if dg is None else dg.to(g.dtype), None, None, None, None, None)
+        if dg is not None:
+            dg = dg.to(ctx.g_dtype)
+            if len(ctx.g_shape) == 3:
+                dg = dg.unsqueeze(-1)
+        return (dx, dw, db, dg, None, None, None, None, None, None)
 
 
-def conv1d_gate(module: nn.Module, x: torch.Tensor, g, in_slope: float = 1.0):
+def cond_f32(g: torch.Tensor | None):
+    """fp32 copy of a 16-bit cond tensor (every layer's slice then feeds the
+    fused gate's fp32 epilogue without a cast of its own), or None when the
+    fused gate does not run (its callers keep the 16-bit slices)."""
+    if (g is None or not GATE_FUSED or not g.is_cuda
+            or g.dtype not in (torch.float16, torch.bfloat16)):
+        return None
+    return g.float()
+
+
+def conv1d_gate(module: nn.Module, x: torch.Tensor, g, in_slope: float = 1.0, g16=None):
     """gate(module(leaky_relu(x, in_slope)), g) (WN / ResBlock2, the conv's
     output feeding only the gate) as one ConvGateHip16 launch inside a 16-bit
     autocast region on a ROCm device; None when that does not apply (the
@@ -1198,6 +1222,9 @@ def conv1d_gate(module: nn.Module, x: torch.Tensor, g, in_slope: float = 1.0):
     w = weight_norm_effective(module)
     ent = _PREPACK.get(module)
     pre = ent[1] if (ent is not None and ent[0] is w and ent[2] == wdt and ent[3]) else None
-    return ConvGateHip16.apply(x if x.dtype == t16 else x.to(t16), w, module.bias,
-                               None if g is None else g.to(t16), module.dilation[0],
-                               module.padding[0], in_slope, wdt, pre)
+    if g is not None and g16 is None:
+        g = g.to(t16)  # (the reference's cond is an autocast op's 16-bit output)
+    if g16 is not None and g16.dtype != t16:
+        g16 = None
+    return ConvGateHip16.apply(x if x.dtype == t16 else x.to(t16), w, module.bias, g,
+                               module.dilation[0], module.padding[0], in_slope, wdt, pre, g16)
