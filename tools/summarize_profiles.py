@@ -31,7 +31,7 @@ for r in stats:
     name = r["Name"]
     short = name.replace("(anonymous namespace)::", "").replace("void ", "")
     key = ("conv1d_mfma_kernel" if "conv1d_mfma_kernel" in name else
-           "resblock_pair_kernel" if "resblock_pair_kernel" in name else
+           "resblock_pair_kernel" if ("resblock_pair_kernel" in name or "resblock16_kernel" in name) else
            short.split("(")[0].split("<")[0][:60])
     fam[key][0] += int(r["Calls"])
     fam[key][1] += float(r["TotalDurationNs"])
@@ -45,7 +45,7 @@ def pmc(name):
     # the bench's dominant kernel: every conv launch of the step (the conv
     # kernel and the fused ResBlock2 pair kernel)
     vals = [float(r["Counter_Value"]) for r in rows
-            if "conv1d_mfma_kernel" in r["Kernel_Name"] or "resblock_pair_kernel" in r["Kernel_Name"]]
+            if any(k in r["Kernel_Name"] for k in ("conv1d_mfma_kernel", "resblock_pair_kernel", "resblock16_kernel"))]
     return vals
 
 
