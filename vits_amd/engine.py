@@ -275,9 +275,8 @@ class GeneratorPlan:
                 cur = dst
                 continue
             # last pair of every branch: accumulate the mean, in branch order
-            descs = grouped(c1_desc(j, p) for j in cj)
-            if descs:
-                ops.conv1d_launch_seq(descs, B, dev)
+            if cj:  # (an empty group would be an empty launch)
+                ops.conv1d_launch_seq(grouped(c1_desc(j, p) for j in cj), B, dev)
             for j in range(nk):
                 kw = dict(accumulate=j > 0, post_div=float(nk) if j == nk - 1 else 1.0)
                 if fused[j][p]:
