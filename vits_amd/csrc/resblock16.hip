@@ -123,10 +123,24 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   const int nb = xcols >> 2;             // 4-step blocks
   const float slope = p.in_slope;
   {
-    const int nunits = (C / 4) * nb;
+    // unit u -> (channel quad cq, 4-step block tb).  kc1 == 1 (A/B switch):
+    // 16 consecutive blocks of one quad per 16 lanes (128-byte global
+    // segments per channel row); otherwise quads fastest (distinct LDS
+    // banks for the 8-byte writes, 32-byte global segments)
+    const bool tfast = p.kc1 == 1;
+    const int nunits = tfast ? (C / 4) * ((nb + 15) >> 4) * 16 : (C / 4) * nb;
     for (int u = tid; u < nunits; u += 256) {
-      const int cq = u % (C / 4);        // channel quad (fastest: distinct LDS banks)
-      const int tb = u / (C / 4);
+      int cq, tb;
+      if (tfast) {
+        const int grp = u >> 4;          // 16-lane group: one quad, 16 blocks
+        const int nbg = (nb + 15) >> 4;  // block groups per quad
+        cq = grp / nbg;
+        tb = 16 * (grp - cq * nbg) + (u & 15);
+        if (cq >= C / 4 || tb >= nb) continue;
+      } else {
+        cq = u % (C / 4);
+        tb = u / (C / 4);
+      }
       const int tt = xstart + 4 * tb;
       const bool ok = tt >= 0 && tt < Tn;  // T % 4 == 0: a block is all in or all out
       t4 v[4];
