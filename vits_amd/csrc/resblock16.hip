@@ -123,45 +123,44 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   const int nb = xcols >> 2;             // 4-step blocks
   const float slope = p.in_slope;
   {
-    // unit u -> (channel quad cq, 4-step block tb).  kc1 == 1 (A/B switch):
-    // 16 consecutive blocks of one quad per 16 lanes (128-byte global
-    // segments per channel row); otherwise quads fastest (distinct LDS
-    // banks for the 8-byte writes, 32-byte global segments)
-    const bool tfast = p.kc1 == 1;
-    const int nunits = tfast ? (C / 4) * ((nb + 15) >> 4) * 16 : (C / 4) * nb;
-    for (int u = tid; u < nunits; u += 256) {
-      int cq, tb;
-      if (tfast) {
-        const int grp = u >> 4;          // 16-lane group: one quad, 16 blocks
-        const int nbg = (nb + 15) >> 4;  // block groups per quad
-        cq = grp / nbg;
-        tb = 16 * (grp - cq * nbg) + (u & 15);
-        if (cq >= C / 4 || tb >= nb) continue;
-      } else {
-        cq = u % (C / 4);
-        tb = u / (C / 4);
-      }
-      const int tt = xstart + 4 * tb;
-      const bool ok = tt >= 0 && tt < Tn;  // T % 4 == 0: a block is all in or all out
-      t4 v[4];
+    // unit u -> (channel quad cq, 4-step block tb), quads fastest (distinct
+    // LDS banks for the 8-byte writes).  Every unit's four 8-byte loads are
+    // issued before any is consumed (NU units per thread in registers): a
+    // load -> convert -> store loop waits one memory round trip per unit.
+    constexpr int NU = ((C / 4) * ((R16_NG + 96 + 6) / 4) + 255) / 256;
+    const int nunits = (C / 4) * nb;
+    // (loads are unconditional - out-of-range units read the utterance's
+    // first block and are zeroed below - so no branch splits the batch)
+    t4 v[NU][4];
+    bool okq[NU];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (ok) {
-          v[i] = *reinterpret_cast<const t4*>(xb + (int64_t)(4 * cq + i) * p.x_cstride + tt);
-        } else {
-          v[i] = t4{};
+    for (int q = 0; q < NU; ++q) {
+      const int u = tid + 256 * q;
+      const int cq = u % (C / 4);
+      const int tt = xstart + 4 * (u / (C / 4));
+      okq[q] = u < nunits && tt >= 0 && tt < Tn;  // T % 4 == 0: a block is all in or out
+      const int64_t off = okq[q] ? (int64_t)(4 * cq) * p.x_cstride + tt : 0;
+      const int64_t cs = okq[q] ? p.x_cstride : 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[q][i] = *reinterpret_cast<const t4*>(xb + off + i * cs);
+    }
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const int u = tid + 256 * q;
+      if (u < nunits) {
+        const int cq = u % (C / 4);
+        const int tb = u / (C / 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          t4 w;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float f = okq[q] ? (float)v[q][i][e] : 0.f;
+            f = f < 0.f ? f * slope : f;
+            w[i] = (T)f;
+          }
+          *reinterpret_cast<t4*>(xs + (4 * tb + e) * XP + 4 * cq) = w;
         }
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        t4 w;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float f = (float)v[i][e];
-          f = f < 0.f ? f * slope : f;
-          w[i] = (T)f;
-        }
-        *reinterpret_cast<t4*>(xs + (4 * tb + e) * XP + 4 * cq) = w;
       }
     }
   }
@@ -267,7 +266,9 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   // ---------------- phase 2: c2 from G --------------------------------------
   gemm(reinterpret_cast<const T*>(p.w2), p.m_pad2, S2 * k, gs, GP, wn, 1);
 
-  // residual (+ running branch mean) epilogue, 16-bit out
+  // residual (+ running branch mean) epilogue, 16-bit out.  The residual /
+  // running-mean loads of a 32x32 tile are issued unconditionally (clamped
+  // to column 0 outside the tile) before any is used.
   T* yb = reinterpret_cast<T*>(p.y) + (int64_t)b * p.y_bstride;
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
@@ -275,15 +276,29 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
     for (int ni = 0; ni < TN; ++ni) {
       const int col = wn + ni * 32 + l32;
       const int t = n0 + col;
-      if (col < BN && t < Tn) {
+      const bool st = col < BN && t < Tn;
+      const int tc = st ? t : 0;
+      float rv[16], yo[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+        rv[r] = (float)xb[(int64_t)row * p.x_cstride + tc];
+      }
+      if (p.accumulate) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
-          float v = (float)xb[(int64_t)row * p.x_cstride + t] + (acc[mi][ni][r] + erow[C + row]);
-          const int64_t di = (int64_t)row * p.y_cstride + t;
-          if (p.accumulate) v = (float)yb[di] + v;
+          yo[r] = (float)yb[(int64_t)row * p.y_cstride + tc];
+        }
+      }
+      if (st) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+          float v = rv[r] + (acc[mi][ni][r] + erow[C + row]);
+          if (p.accumulate) v = yo[r] + v;
           if (p.post_div != 1.0f) v = v / p.post_div;
-          yb[di] = (T)(t < L ? v : 0.f);
+          yb[(int64_t)row * p.y_cstride + t] = (T)(t < L ? v : 0.f);
         }
       }
     }

@@ -674,9 +674,6 @@ def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch
 # fused pairs of 16-bit models (csrc/resblock16.hip): VITS_FUSED_PAIRS16=0
 # keeps their two-conv path
 FUSED_PAIRS16 = os.environ.get("VITS_FUSED_PAIRS16", "1") != "0"
-# window staging map of resblock16 (kc1 field): 1 = time blocks fastest
-# (coalesced 128-byte rows), 16 = channel quads fastest (A/B switch)
-R16_MAP = int(os.environ.get("VITS_R16_MAP", "16"))
 
 
 def resblock_pair16_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -> bool:
@@ -702,7 +699,7 @@ def resblock_pair16_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: tor
     d = ResblockPairDesc()
     d.x, d.x_bstride, d.x_cstride, d.t_len = x.data_ptr(), x.stride(0), x.stride(1), T
     d.channels, d.in_slope = C_, in_slope
-    d.w1, d.m_pad1, d.cin_pad1, d.kc1 = c1.w.data_ptr(), c1.m_pad, c1.cin_pad, R16_MAP
+    d.w1, d.m_pad1, d.cin_pad1, d.kc1 = c1.w.data_ptr(), c1.m_pad, c1.cin_pad, 16
     d.k, d.dil, d.kc2 = c1.k, c1.dil, 16
     d.b1 = _ptr(c1.bias)
     if cond is not None:
