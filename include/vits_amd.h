@@ -564,6 +564,12 @@ int vits_resblock_pair_kc(int channels, int k, int dil, int* kc1, int* kc2);
 /* (k - 1) * dil <= 96, T % 4 == 0.                                       */
 int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch, int wdtype,
                                  void* stream);
+/* The last pairs of a stage's n branches as ONE launch: d[0].y receives  */
+/* (sum_i pair_i(d[i].x)) / n (models.py:311-313's branch mean; each      */
+/* workgroup runs every member on its time tile and sums in registers);   */
+/* the members share t_len and lengths; accumulate / post_div ignored.    */
+int vits_resblock_pair16_mean_forward(const vits_resblock_pair_desc* d, int n, int batch,
+                                      int wdtype, void* stream);
 
 /* Fused RAdam step (radam.py:35-99, the D optimizer of train_stft.py:97) */
 /* over a list of fp32 tensors, one launch per VITS_RADAM_MAX tensors.     */

@@ -577,6 +577,13 @@ def test_resblock_pair16_fused(device, C, k, dil, T, wdt):
             B, device, wdt)
     torch.cuda.synchronize()
     _close(acc, (refs[0] + refs[1] + refs[2]) / 3, tol=2 * tol, what="mean")
+    # the branch mean as ONE launch (vits_resblock_pair16_mean_forward)
+    mean = torch.full((B, C, T), float("nan"), device=device, dtype=dt)
+    ops.resblock_pair16_launch(tuple(
+        ops.resblock_pair16_desc(c1, c2, xs[j], mean, cond=cd)
+        for j, (c1, c2, cd) in enumerate(packs)), B, device, wdt, mean=True)
+    torch.cuda.synchronize()
+    _close(mean, (refs[0] + refs[1] + refs[2]) / 3, tol=tol, what="mean launch")
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])

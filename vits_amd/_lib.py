@@ -354,6 +354,8 @@ _SIGS = {
         C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vits_resblock_pair16_forward": (
         C.c_int, [C.POINTER(ResblockPairDesc), C.c_int, C.c_int, C.c_int, C.c_void_p]),
+    "vits_resblock_pair16_mean_forward": (
+        C.c_int, [C.POINTER(ResblockPairDesc), C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "vits_gate_forward_io16": (
         C.c_int,
         [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32,

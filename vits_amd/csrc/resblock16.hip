@@ -42,6 +42,12 @@ struct R16Group {
   vits_resblock_pair_desc d[R16_GROUP];
   int n;
   int batch;
+  // mean: ONE output, the mean of the n members' pair outputs (the last
+  // pairs of a stage's branches, models.py:311-313): each workgroup runs
+  // every member on its time tile (tile width bn, common to the members)
+  // and keeps the running sum in registers; d[0] names the output
+  int mean;
+  int bn;
 };
 
 __device__ __forceinline__ float r16_sigmoid(float x) {
@@ -62,7 +68,7 @@ __host__ __device__ inline int r16_lds_bytes(int C, int k, int dil) {
   return 2 * (r16_xcols(k, dil) * xp + (R16_NG + 16) * gp) + 4 * 2 * C + 64;
 }
 
-template <int C, typename T>
+template <int C, typename T, bool MEAN>
 __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   constexpr int H = C / 2;
   constexpr int TM = C / 32;       // 32-row MFMA tiles of c1 / c2 (one wave row)
@@ -75,31 +81,47 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   typedef T t4 __attribute__((ext_vector_type(4)));
   static_assert(C == 32 || C == 64, "32- / 64-channel stages");
 
-  const int gi = (int)blockIdx.z / G.batch;
-  const vits_resblock_pair_desc& p = G.d[gi];
-  const int b = (int)blockIdx.z - gi * G.batch;
-  const int k = p.k;
-  const int dil = p.dil;
-  const int Tn = p.t_len;
-  const int L = p.lengths ? min(Tn, (int)p.lengths[b]) : Tn;
-  const int p1 = (k - 1) * dil / 2;
-  const int p2 = (k - 1) / 2;
-  const int BN = R16_NG - 2 * p2;
+  const int gsel = MEAN ? 0 : (int)blockIdx.z / G.batch;
+  const int b = (int)blockIdx.z - gsel * G.batch;
+  const vits_resblock_pair_desc& p0 = G.d[gsel];
+  const int Tn = p0.t_len;
+  const int L = p0.lengths ? min(Tn, (int)p0.lengths[b]) : Tn;
+  const int BN = MEAN ? G.bn : R16_NG - (p0.k - 1);
   const int n0 = blockIdx.x * BN;
   if (n0 >= Tn) return;
-  if (p.lengths && p.len_skip > 0 && n0 >= L + p.len_skip) return;
+  if (p0.lengths && p0.len_skip > 0 && n0 >= L + p0.len_skip) return;
 
   extern __shared__ float smem[];
   float* const erow = smem;                                   // [2C] row constants
   T* const xs = reinterpret_cast<T*>(smem + 2 * C + 16);      // [xcols][XP]
-  const int xcols = r16_xcols(k, dil);
-  T* const gs = xs + xcols * XP;                              // [NG + 16][GP]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wn = (tid >> 6) * 64;
   const int l32 = lane & 31;
   const int lhi = lane >> 5;
+
+  f32x16 acc[TM][TN];
+  f32x16 ysum[MEAN ? TM : 1][MEAN ? TN : 1];  // (MEAN: the running branch sum)
+  if constexpr (MEAN) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ysum[i][j][r] = 0.f;
+  }
+
+  const int nmem = MEAN ? G.n : 1;
+  for (int mem = 0; mem < nmem; ++mem) {
+  const vits_resblock_pair_desc& p = G.d[gsel + mem];
+  const int k = p.k;
+  const int dil = p.dil;
+  const int p1 = (k - 1) * dil / 2;
+  const int p2 = (k - 1) / 2;
+  const int xcols = r16_xcols(k, dil);
+  T* const gs = xs + xcols * XP;                              // [NG + 16][GP]
+  if (mem > 0) __syncthreads();  // the previous member's reads of LDS are done
 
   // row constants: c1 bias + cond (gate-interleaved order), c2 bias
   const float* cond = p.cond ? p.cond + (int64_t)b * p.cond_bstride : nullptr;
@@ -166,7 +188,6 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   }
   __syncthreads();
 
-  f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -269,7 +290,6 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   // residual (+ running branch mean) epilogue, 16-bit out.  The residual /
   // running-mean loads of a 32x32 tile are issued unconditionally (clamped
   // to column 0 outside the tile) before any is used.
-  T* yb = reinterpret_cast<T*>(p.y) + (int64_t)b * p.y_bstride;
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
@@ -278,12 +298,22 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
       const int t = n0 + col;
       const bool st = col < BN && t < Tn;
       const int tc = st ? t : 0;
-      float rv[16], yo[16];
+      float rv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
         rv[r] = (float)xb[(int64_t)row * p.x_cstride + tc];
       }
+      if constexpr (MEAN) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+          ysum[mi][ni][r] += rv[r] + (acc[mi][ni][r] + erow[C + row]);
+        }
+        continue;
+      }
+      T* yb = reinterpret_cast<T*>(p.y) + (int64_t)b * p.y_bstride;
+      float yo[16];
       if (p.accumulate) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -303,6 +333,27 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
       }
     }
   }
+  }  // members
+
+  if constexpr (MEAN) {
+    const float inv_n = 1.0f / (float)G.n;
+    T* yb = reinterpret_cast<T*>(p0.y) + (int64_t)b * p0.y_bstride;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int col = wn + ni * 32 + l32;
+        const int t = n0 + col;
+        if (col < BN && t < Tn) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+            yb[(int64_t)row * p0.y_cstride + t] = (T)(t < L ? ysum[mi][ni][r] * inv_n : 0.f);
+          }
+        }
+      }
+    }
+  }
 }
 
 template <int C, typename T>
@@ -312,12 +363,17 @@ int r16_launch(const R16Group& g, hipStream_t s) {
     const vits_resblock_pair_desc& d = g.d[i];
     const int l = r16_lds_bytes(C, d.k, d.dil);
     if (l > lds) lds = l;
-    const int BN = R16_NG - (d.k - 1);
+    const int BN = g.mean ? g.bn : R16_NG - (d.k - 1);
     const int x = (d.t_len + BN - 1) / BN;
     if (x > gx) gx = x;
   }
   if (lds > 160 * 1024) return VITS_E_UNSUP;
-  hipLaunchKernelGGL((resblock16_kernel<C, T>), dim3(gx, 1, g.n * g.batch), dim3(256), lds, s, g);
+  if (g.mean)
+    hipLaunchKernelGGL((resblock16_kernel<C, T, true>), dim3(gx, 1, g.batch), dim3(256), lds, s,
+                       g);
+  else
+    hipLaunchKernelGGL((resblock16_kernel<C, T, false>), dim3(gx, 1, g.n * g.batch), dim3(256),
+                       lds, s, g);
   return vits_launch_status();
 }
 
@@ -343,22 +399,42 @@ int r16_check(const vits_resblock_pair_desc& d) {
 
 }  // namespace
 
-extern "C" int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch,
-                                            int wdtype, void* stream) {
+static int r16_run(const vits_resblock_pair_desc* d, int n, int batch, int wdtype, int mean,
+                   void* stream) {
   if (!d || n < 1 || n > R16_GROUP || batch < 1) return VITS_E_ARG;
   if (wdtype != VITS_WDT_BF16 && wdtype != VITS_WDT_F16) return VITS_E_ARG;
   R16Group g;
   g.n = n;
   g.batch = batch;
+  g.mean = mean;
+  int kmax = 1;
   for (int i = 0; i < n; ++i) {
     const int rc = r16_check(d[i]);
     if (rc) return rc;
     if (d[i].channels != d[0].channels) return VITS_E_SHAPE;
+    if (mean) {
+      // one output tile per workgroup over every member: same time axis,
+      // the same utterance lengths, and no member may write its input
+      VITS_CHECK_SHAPE(d[i].t_len == d[0].t_len && d[i].lengths == d[0].lengths);
+      VITS_CHECK_ARG(reinterpret_cast<const void*>(d[0].y) != reinterpret_cast<const void*>(d[i].x));
+    }
+    if (d[i].k > kmax) kmax = d[i].k;
     g.d[i] = d[i];
   }
+  g.bn = R16_NG - (kmax - 1);
   hipStream_t s = as_stream(stream);
   const bool f16 = wdtype == VITS_WDT_F16;
   if (d[0].channels == 32)
     return f16 ? r16_launch<32, _Float16>(g, s) : r16_launch<32, __bf16>(g, s);
   return f16 ? r16_launch<64, _Float16>(g, s) : r16_launch<64, __bf16>(g, s);
+}
+
+extern "C" int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch,
+                                            int wdtype, void* stream) {
+  return r16_run(d, n, batch, wdtype, 0, stream);
+}
+
+extern "C" int vits_resblock_pair16_mean_forward(const vits_resblock_pair_desc* d, int n,
+                                                 int batch, int wdtype, void* stream) {
+  return r16_run(d, n, batch, wdtype, 1, stream);
 }

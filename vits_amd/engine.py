@@ -131,6 +131,9 @@ _GROUP_BRANCHES = os.environ.get("VITS_GROUP_BRANCHES", "1") != "0"
 # fused ResBlock2 pairs on the 32/64-channel stages (VITS_FUSED_PAIRS=0: the
 # two-conv path, for A/B timing and the parity test of both)
 _FUSED_PAIRS = os.environ.get("VITS_FUSED_PAIRS", "1") != "0"
+# 16-bit models: the last pairs of a stage's branches as one branch-mean
+# launch (vits_resblock_pair16_mean_forward); 0 = one accumulating launch each
+MEAN_PAIRS16 = os.environ.get("VITS_MEAN_PAIRS16", "1") != "0"
 # 16-bit models keep the decoder's activations 16-bit in HBM (as the
 # reference's .half() model holds them): every conv of the Generator reads and
 # writes its own 16-bit type (io16), halving the stage traffic.  C5 (B=4,
@@ -275,6 +278,11 @@ class GeneratorPlan:
                 cur = dst
                 continue
             # last pair of every branch: accumulate the mean, in branch order
+            if io16 and not cj and 1 < nk <= 3 and MEAN_PAIRS16:
+                # every branch fused: one launch sums them in registers
+                ops.resblock_pair16_launch(tuple(pair_desc(j, p, xs) for j in range(nk)), B,
+                                           dev, blocks[0][0][0].wdtype, mean=True)
+                continue
             if cj:  # (an empty group would be an empty launch)
                 ops.conv1d_launch_seq(grouped(c1_desc(j, p) for j in cj), B, dev)
             for j in range(nk):

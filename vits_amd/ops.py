@@ -574,7 +574,7 @@ class ConvTimer:
         self.shapes.append("conv " + "+".join(
             f"m{d.m}c{d.cin}k{d.k}d{d.dil}T{d.n_out}e{d.epi}t{d.tile}" for d in group))
 
-    def launch_pairs(self, lib, group, batch, device, wdtype=None):
+    def launch_pairs(self, lib, group, batch, device, wdtype=None, mean=False):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         stream = torch.cuda.current_stream(device)
@@ -584,8 +584,8 @@ class ConvTimer:
             check(lib.vits_resblock_pair_forward(arr, len(group), batch, stream.cuda_stream),
                   "vits_resblock_pair_forward")
         else:
-            check(lib.vits_resblock_pair16_forward(arr, len(group), batch, int(wdtype),
-                                                   stream.cuda_stream),
+            fn = lib.vits_resblock_pair16_mean_forward if mean else lib.vits_resblock_pair16_forward
+            check(fn(arr, len(group), batch, int(wdtype), stream.cuda_stream),
                   "vits_resblock_pair16_forward")
         e.record(stream)
         self.records.append((s, e, sum(resblock_pair_flops(d, batch) for d in group)))
@@ -713,15 +713,19 @@ def resblock_pair16_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: tor
     return d
 
 
-def resblock_pair16_launch(descs, batch: int, device: torch.device, wdtype: int):
-    """One launch of up to 3 independent 16-bit pairs (tuple) or one pair."""
+def resblock_pair16_launch(descs, batch: int, device: torch.device, wdtype: int,
+                           mean: bool = False):
+    """One launch of up to 3 independent 16-bit pairs (tuple) or one pair;
+    mean=True: the members' mean into descs[0]'s output
+    (vits_resblock_pair16_mean_forward)."""
     group = tuple(descs) if isinstance(descs, (tuple, list)) else (descs,)
     lib = _lib.load()
     if ConvTimer.active is not None:
-        return ConvTimer.active.launch_pairs(lib, group, batch, device, wdtype)
+        return ConvTimer.active.launch_pairs(lib, group, batch, device, wdtype, mean=mean)
     arr = (ResblockPairDesc * len(group))(*group)
-    check(lib.vits_resblock_pair16_forward(arr, len(group), batch, int(wdtype),
-                                           _stream_ptr(device)), "vits_resblock_pair16_forward")
+    fn = lib.vits_resblock_pair16_mean_forward if mean else lib.vits_resblock_pair16_forward
+    check(fn(arr, len(group), batch, int(wdtype), _stream_ptr(device)),
+          "vits_resblock_pair16_forward")
 
 
 def resblock_pair_flops(d: ResblockPairDesc, batch: int) -> int:
