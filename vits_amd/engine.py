@@ -132,7 +132,9 @@ _GROUP_BRANCHES = os.environ.get("VITS_GROUP_BRANCHES", "1") != "0"
 # two-conv path, for A/B timing and the parity test of both)
 _FUSED_PAIRS = os.environ.get("VITS_FUSED_PAIRS", "1") != "0"
 # 16-bit models: the last pairs of a stage's branches as one branch-mean
-# launch (vits_resblock_pair16_mean_forward); 0 = one accumulating launch each
+# launch (vits_resblock_pair16_mean_forward); 0 = one accumulating launch each.
+# Used on the 32-channel stage (C5: 0.47 -> 0.41 ms); on the 64-channel one
+# the summing kernel reaches 256 VGPRs and lost (0.61 -> 0.69 ms)
 MEAN_PAIRS16 = os.environ.get("VITS_MEAN_PAIRS16", "1") != "0"
 # 16-bit models keep the decoder's activations 16-bit in HBM (as the
 # reference's .half() model holds them): every conv of the Generator reads and
@@ -278,7 +280,7 @@ class GeneratorPlan:
                 cur = dst
                 continue
             # last pair of every branch: accumulate the mean, in branch order
-            if io16 and not cj and 1 < nk <= 3 and MEAN_PAIRS16:
+            if io16 and not cj and 1 < nk <= 3 and MEAN_PAIRS16 and C == 32:
                 # every branch fused: one launch sums them in registers
                 ops.resblock_pair16_launch(tuple(pair_desc(j, p, xs) for j in range(nk)), B,
                                            dev, blocks[0][0][0].wdtype, mean=True)
