@@ -532,7 +532,7 @@ def test_resblock_pair_fused(device, C, k, dil, T):
 
 @pytest.mark.parametrize("C,k,dil,T", [
     (32, 3, 1, 12), (32, 11, 5, 300), (64, 7, 3, 2052), (64, 3, 5, 48), (32, 7, 1, 9216),
-    (64, 11, 5, 1000), (64, 11, 1, 500),
+    (64, 11, 5, 1000), (64, 11, 1, 500), (128, 3, 1, 500), (128, 11, 5, 1000), (128, 7, 3, 124),
 ])
 @pytest.mark.parametrize("wdt", [ops.WDT_BF16, ops.WDT_F16])
 def test_resblock_pair16_fused(device, C, k, dil, T, wdt):

@@ -37,7 +37,10 @@
 namespace {
 
 constexpr int R16_GROUP = 3;
-constexpr int R16_NG = 256;  // phase-1 columns per tile (4 waves x 64)
+// phase-1 columns per tile: 256 for C = 32 / 64 (4 waves x 64 columns),
+// 128 for C = 128 (2 x 2 waves of 64 rows x 64 columns: the 128-channel
+// window and gated tile fit two workgroups per CU)
+__host__ __device__ constexpr int r16_ng(int C) { return C == 128 ? 128 : 256; }
 struct R16Group {
   vits_resblock_pair_desc d[R16_GROUP];
   int n;
@@ -59,34 +62,38 @@ __device__ __forceinline__ float r16_tanh(float x) {
 
 // LDS geometry (host and device agree): window columns (4-aligned), row
 // pitches in elements, bytes of the whole workgroup
-__host__ __device__ inline int r16_xcols(int k, int dil) {
+__host__ __device__ inline int r16_xcols(int NG, int k, int dil) {
   // NG + (k-1) dil window columns + up to 3 of alignment shift, 4-blocks
-  return ((R16_NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
+  return ((NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
 }
 __host__ __device__ inline int r16_lds_bytes(int C, int k, int dil) {
-  const int xp = C + 8, gp = C / 2 + 8;
-  return 2 * (r16_xcols(k, dil) * xp + (R16_NG + 16) * gp) + 4 * 2 * C + 64;
+  const int xp = C + 8, gp = C / 2 + 8, NG = r16_ng(C);
+  return 2 * (r16_xcols(NG, k, dil) * xp + (NG + 16) * gp) + 4 * 2 * C + 64;
 }
 
 template <int C, typename T, bool MEAN>
 __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   constexpr int H = C / 2;
-  constexpr int TM = C / 32;       // 32-row MFMA tiles of c1 / c2 (one wave row)
-  constexpr int TN = 2;            // 4 waves x 64 columns
+  constexpr int NG = r16_ng(C);
+  constexpr int WAVES_M = C == 128 ? 2 : 1;
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int TM = C / 32 / WAVES_M;  // 32-row MFMA tiles of c1 / c2 per wave
+  constexpr int TN = 2;                 // 64 columns per wave
+  static_assert(NG == 64 * WAVES_N, "tile columns");
   constexpr int XP = C + 8;        // window row pitch (16-bit elements)
   constexpr int GP = H + 8;        // gated row pitch
   constexpr int S1 = C / 16;       // 16-channel slabs of c1's K
   constexpr int S2 = H / 16;       // ... of c2's K
   typedef T t8 __attribute__((ext_vector_type(8)));
   typedef T t4 __attribute__((ext_vector_type(4)));
-  static_assert(C == 32 || C == 64, "32- / 64-channel stages");
+  static_assert(C == 32 || C == 64 || C == 128, "32- / 64- / 128-channel stages");
 
   const int gsel = MEAN ? 0 : (int)blockIdx.z / G.batch;
   const int b = (int)blockIdx.z - gsel * G.batch;
   const vits_resblock_pair_desc& p0 = G.d[gsel];
   const int Tn = p0.t_len;
   const int L = p0.lengths ? min(Tn, (int)p0.lengths[b]) : Tn;
-  const int BN = MEAN ? G.bn : R16_NG - (p0.k - 1);
+  const int BN = MEAN ? G.bn : NG - (p0.k - 1);
   const int n0 = blockIdx.x * BN;
   if (n0 >= Tn) return;
   if (p0.lengths && p0.len_skip > 0 && n0 >= L + p0.len_skip) return;
@@ -97,7 +104,9 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wn = (tid >> 6) * 64;
+  const int wid = tid >> 6;
+  const int wn = (wid % WAVES_N) * 64;   // wave's column offset
+  const int wm = (wid / WAVES_N) * (C / WAVES_M);  // wave's row offset
   const int l32 = lane & 31;
   const int lhi = lane >> 5;
 
@@ -119,7 +128,7 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   const int dil = p.dil;
   const int p1 = (k - 1) * dil / 2;
   const int p2 = (k - 1) / 2;
-  const int xcols = r16_xcols(k, dil);
+  const int xcols = r16_xcols(NG, k, dil);
   T* const gs = xs + xcols * XP;                              // [NG + 16][GP]
   if (mem > 0) __syncthreads();  // the previous member's reads of LDS are done
 
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
     // LDS banks for the 8-byte writes).  Every unit's four 8-byte loads are
     // issued before any is consumed (NU units per thread in registers): a
     // load -> convert -> store loop waits one memory round trip per unit.
-    constexpr int NU = ((C / 4) * ((R16_NG + 96 + 6) / 4) + 255) / 256;
+    constexpr int NU = ((C / 4) * ((NG + 96 + 6) / 4) + 255) / 256;
     const int nunits = (C / 4) * nb;
     // (loads are unconditional - out-of-range units read the utterance's
     // first block and are zeroed below - so no branch splits the batch)
@@ -208,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   // col0 + ni * 32 + j * jstride
   auto gemm = [&](const T* wimg, int m_pad, int nsteps, const T* bsrc, int pitch, int col0,
                   int jstride) {
-    const T* wl = wimg + ((int64_t)lhi * m_pad + l32) * 8;
+    const T* wl = wimg + ((int64_t)lhi * m_pad + wm + l32) * 8;
     const int64_t wstep = (int64_t)16 * m_pad;
     const T* bl = bsrc + (col0 + l32) * pitch + 8 * lhi;
     auto loadA = [&](int s, t8* a) {
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
 #pragma unroll
       for (int r = 0; r < 16; r += 4) {
         // rows rloc, rloc + 1 (a_q, b_q) and rloc + 2, rloc + 3 (a_q+1, b_q+1)
-        const int row = mi * 32 + 4 * lhi + 8 * (r >> 2);
+        const int row = wm + mi * 32 + 4 * lhi + 8 * (r >> 2);
         const float g0 = r16_tanh(acc[mi][ni][r] + erow[row]) *
                          r16_sigmoid(acc[mi][ni][r + 1] + erow[row + 1]);
         const float g1 = r16_tanh(acc[mi][ni][r + 2] + erow[row + 2]) *
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
     }
   }
-  for (int i = tid; i < 16 * H; i += 256) gs[(R16_NG + i / H) * GP + i % H] = (T)0.f;
+  for (int i = tid; i < 16 * H; i += 256) gs[(NG + i / H) * GP + i % H] = (T)0.f;
   __syncthreads();
 
   // ---------------- phase 2: c2 from G --------------------------------------
@@ -301,13 +310,13 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
       float rv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+        const int row = wm + mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
         rv[r] = (float)xb[(int64_t)row * p.x_cstride + tc];
       }
       if constexpr (MEAN) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+          const int row = wm + mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
           ysum[mi][ni][r] += rv[r] + (acc[mi][ni][r] + erow[C + row]);
         }
         continue;
@@ -317,14 +326,14 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
       if (p.accumulate) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+          const int row = wm + mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
           yo[r] = (float)yb[(int64_t)row * p.y_cstride + tc];
         }
       }
       if (st) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+          const int row = wm + mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
           float v = rv[r] + (acc[mi][ni][r] + erow[C + row]);
           if (p.accumulate) v = yo[r] + v;
           if (p.post_div != 1.0f) v = v / p.post_div;
@@ -347,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
         if (col < BN && t < Tn) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int row = mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
+            const int row = wm + mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
             yb[(int64_t)row * p0.y_cstride + t] = (T)(t < L ? ysum[mi][ni][r] * inv_n : 0.f);
           }
         }
@@ -363,7 +372,7 @@ int r16_launch(const R16Group& g, hipStream_t s) {
     const vits_resblock_pair_desc& d = g.d[i];
     const int l = r16_lds_bytes(C, d.k, d.dil);
     if (l > lds) lds = l;
-    const int BN = g.mean ? g.bn : R16_NG - (d.k - 1);
+    const int BN = g.mean ? g.bn : r16_ng(C) - (d.k - 1);
     const int x = (d.t_len + BN - 1) / BN;
     if (x > gx) gx = x;
   }
@@ -381,7 +390,7 @@ int r16_check(const vits_resblock_pair_desc& d) {
   VITS_CHECK_ARG(d.x && d.w1 && d.w2 && d.y);
   // other workgroups still read x (halos, residual): never write in place
   VITS_CHECK_ARG(reinterpret_cast<const void*>(d.y) != reinterpret_cast<const void*>(d.x));
-  VITS_CHECK_SHAPE(d.channels == 32 || d.channels == 64);
+  VITS_CHECK_SHAPE(d.channels == 32 || d.channels == 64 || d.channels == 128);
   VITS_CHECK_SHAPE(d.k >= 1 && d.k <= 15 && (d.k & 1) == 1 && d.dil >= 1 && d.t_len > 0);
   VITS_CHECK_SHAPE((d.k - 1) * d.dil <= 96);  // window within the LDS budget
   // images: [cin_pad/16][k][2][m_pad][8], rows = C (c1 gate-interleaved / c2)
@@ -421,12 +430,14 @@ static int r16_run(const vits_resblock_pair_desc* d, int n, int batch, int wdtyp
     if (d[i].k > kmax) kmax = d[i].k;
     g.d[i] = d[i];
   }
-  g.bn = R16_NG - (kmax - 1);
+  g.bn = r16_ng(d[0].channels) - (kmax - 1);
   hipStream_t s = as_stream(stream);
   const bool f16 = wdtype == VITS_WDT_F16;
   if (d[0].channels == 32)
     return f16 ? r16_launch<32, _Float16>(g, s) : r16_launch<32, __bf16>(g, s);
-  return f16 ? r16_launch<64, _Float16>(g, s) : r16_launch<64, __bf16>(g, s);
+  if (d[0].channels == 64)
+    return f16 ? r16_launch<64, _Float16>(g, s) : r16_launch<64, __bf16>(g, s);
+  return f16 ? r16_launch<128, _Float16>(g, s) : r16_launch<128, __bf16>(g, s);
 }
 
 extern "C" int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch,

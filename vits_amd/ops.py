@@ -682,7 +682,7 @@ def resblock_pair16_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -
     (k - 1) * dil <= 96, 8-byte aligned time rows (T % 4 == 0)."""
     C_ = c2.out_channels
     return (FUSED_PAIRS16 and c1.wdtype in (WDT_BF16, WDT_F16) and c2.wdtype == c1.wdtype
-            and x.dtype == _WDT_TORCH[c1.wdtype] and C_ in (32, 64) and c1.m == C_
+            and x.dtype == _WDT_TORCH[c1.wdtype] and C_ in (32, 64, 128) and c1.m == C_
             and c1.cin == C_ and c2.cin == C_ // 2 and c2.m == C_ and c1.k == c2.k
             and c1.k % 2 == 1 and (c1.k - 1) * c1.dil <= 96 and c2.dil == 1
             and c1.epi == EPI_GATE and x.shape[2] % 4 == 0 and x.stride(2) == 1
