@@ -410,17 +410,22 @@ def _latest_summary(pattern):
         return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
-def train_traffic():
-    """HBM bytes per train step from the newest committed train PMC summary
-    (profiles/<tag>_train_summary.json, tools/summarize_train_profiles.py)."""
+def train_traffic(batch=None):
+    """HBM bytes per train step from the committed train PMC summaries
+    (profiles/<tag>_train_summary.json, tools/summarize_train_profiles.py):
+    the newest one measured at this batch, else the newest (scaled)."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_train_summary.json")))
     if not files:
         return None, None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return (d.get("hbm_bytes_per_step"), d.get("batch"), os.path.relpath(files[-1], ROOT))
+    ds = []
+    for fn in files:
+        with open(fn) as f:
+            ds.append((json.load(f), fn))
+    same = [x for x in ds if x[0].get("batch") == batch]
+    d, fn = (same or ds)[-1]
+    return (d.get("hbm_bytes_per_step"), d.get("batch"), os.path.relpath(fn, ROOT))
 
 
 def train_leg(args, device, rank, world, dist, B=None, cpu_base=True):
@@ -481,13 +486,14 @@ def train_leg(args, device, rank, world, dist, B=None, cpu_base=True):
     # PMC HBM bytes per step (FETCH x2 + WRITE over every kernel of one
     # replayed step, scaled to this batch) from the committed summary
     achieved = TRAIN_GFLOP_PER_UTT * 1e9 * B * args.train_steps / el / 1e12
-    tb, tbatch, tsrc = train_traffic()
+    tb, tbatch, tsrc = train_traffic(B)
     res["roofline"] = {
         "bound": "mfma", "kernel": "whole train_stft step (every kernel of the replayed graph)",
         "achieved": round(achieved, 2), "peak": FP16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / FP16_MFMA_PEAK_TFLOPS, 4),
         "traffic": None if tb is None else int(tb * B / tbatch),
-        "traffic_unit": "HBM bytes per step (PMC, scaled from batch %s)" % tbatch,
+        "traffic_unit": ("HBM bytes per step (PMC at this batch)" if tbatch == B else
+                         "HBM bytes per step (PMC, scaled from batch %s)" % tbatch),
         "traffic_source": tsrc}
     if graph_err:
         res["graph_error"] = graph_err
