@@ -195,7 +195,9 @@ def test_train_step_fused_spectral_norm_matches_torch_hooks():
     assert len(ga) == len(gb) == len(gn) and len(ga) > 100
     fused = max(_rel_l2(a, b) for (_, a), (_, b) in zip(ga, gb))
     floor = max(_rel_l2(a, b) for (_, a), (_, b) in zip(gn, gb))
-    assert fused <= 3 * floor + 1e-3, (fused, floor)
+    worst = sorted(((_rel_l2(a, b), _rel_l2(c, b), n) for (n, a), (_, b), (_, c)
+                    in zip(ga, gb, gn)), reverse=True)[:4]
+    assert fused <= 3 * floor + 1e-3, (fused, floor, worst)
     for i, (a, b) in enumerate(zip(ba, bb)):
         _close(a, b, 2e-3, f"D buffer {i}")
 
@@ -253,4 +255,6 @@ def test_generator_fused_weight_norm_matches_torch_hooks():
     assert len(ga) == len(gb) == len(gn) and len(ga) > 50
     fused = max(_rel_l2(a, b) for (_, a), (_, b) in zip(ga, gb))
     floor = max(_rel_l2(a, b) for (_, a), (_, b) in zip(gn, gb))
-    assert fused <= 3 * floor + 1e-3, (fused, floor)
+    worst = sorted(((_rel_l2(a, b), _rel_l2(c, b), n) for (n, a), (_, b), (_, c)
+                    in zip(ga, gb, gn)), reverse=True)[:4]
+    assert fused <= 3 * floor + 1e-3, (fused, floor, worst)

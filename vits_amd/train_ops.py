@@ -1199,11 +1199,14 @@ class ConvGateHip16(torch.autograd.Function):
         return (dx, dw, db, dg, None, None, None, None, None, None)
 
 
+COND_F32 = os.environ.get("VITS_COND_F32", "1") != "0"  # A/B switch
+
+
 def cond_f32(g: torch.Tensor | None):
     """fp32 copy of a 16-bit cond tensor (every layer's slice then feeds the
     fused gate's fp32 epilogue without a cast of its own), or None when the
     fused gate does not run (its callers keep the 16-bit slices)."""
-    if (g is None or not GATE_FUSED or not g.is_cuda
+    if (g is None or not GATE_FUSED or not COND_F32 or not g.is_cuda
             or g.dtype not in (torch.float16, torch.bfloat16)):
         return None
     return g.float()
