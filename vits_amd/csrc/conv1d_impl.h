@@ -1048,7 +1048,40 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
         OutDesc o1{p.out1.y, p.out1.y_bstride, p.out1.y_cstride, p.out1.act, p.out1.res,
                    p.out1.res_bstride, p.out1.res_cstride, p.out1.res_scale,
                    p.out1.accumulate, p.out1.post_div};
-        if (n < p.n_out) {
+        // the 16 rows of a 32x32 sub-tile lie in one 32-row block: when that
+        // block is on one side of the split (split % 32 == 0: every WN
+        // res_skip layer), every residual / accumulator load of the
+        // sub-tile is issued before the first store (store_std per element
+        // waited one memory round trip per row)
+        const int blk = rbase - 4 * lhi;
+        if (n < p.n_out && (blk + 32 <= p.split || blk >= p.split)) {
+          const bool s1 = blk >= p.split;
+          const OutDesc& o = s1 ? o1 : o0;
+          const int cofs = s1 ? p.split : 0;
+          float v[16], rv[16], yo[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            v[r] = apply_act(acc[mi][ni][r] + erow[rloc + (r & 3) + 8 * (r >> 2)], o.act);
+          const int64_t rb = (int64_t)b * o.res_bstride + n;
+          const int64_t yb = (int64_t)b * o.y_bstride + n;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + (r & 3) + 8 * (r >> 2);
+            const int ch = row < p.m ? row - cofs : 0;
+            rv[r] = o.res ? ld_io<io_t>(o.res, rb + (int64_t)ch * o.res_cstride) : 0.f;
+            yo[r] = o.accumulate ? ld_io<io_t>(o.y, yb + (int64_t)ch * o.y_cstride) : 0.f;
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + (r & 3) + 8 * (r >> 2);
+            float t = v[r];
+            if (o.res) t = rv[r] + o.res_scale * t;
+            if (o.accumulate) t = yo[r] + t;
+            if (o.post_div != 1.0f) t = t / o.post_div;
+            if (n >= len_b) t = 0.f;
+            if (row < p.m) st_io<io_t>(o.y, yb + (int64_t)(row - cofs) * o.y_cstride, t);
+          }
+        } else if (n < p.n_out) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int ro = (r & 3) + 8 * (r >> 2);
