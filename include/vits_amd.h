@@ -75,7 +75,6 @@ extern "C" {
 #define VITS_TILE_64x256 1
 #define VITS_TILE_32x256 2
 #define VITS_TILE_64x128 3  /* chosen by the library for small grids of 128x128 layers */
-#define VITS_TILE_96x256 4  /* 16-bit operands only: 96-row layers without a padded row block */
 
 typedef struct vits_conv_out {
   float* y;               /* output [B][*][y_cstride]                        */

@@ -51,8 +51,6 @@ CASES = [
     (2, 1, 64, 1, 1, 0, 1000, 1.0),        # WaveDiscriminator input conv
     (1, 513, 256, 1, 1, 0, 77, 1.0),       # PosteriorEncoder pre (ragged T)
     (2, 160, 160, 5, 4, 0, 301, 0.2),      # MWD scale 3, odd length
-    (2, 96, 96, 5, 3, 0, 1500, 0.2),       # MWD 96-channel layer: the 96x256 tile
-    (3, 96, 96, 5, 9, 0, 1101, 0.2),       # ... ragged T, last tile partial
 ]
 
 

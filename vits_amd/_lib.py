@@ -23,10 +23,9 @@ VITS_E_UNSUP = -3
 
 EPI_STORE, EPI_GATE, EPI_UPSAMPLE = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_EXP = 0, 1, 2, 3
-TILE_128x128, TILE_64x256, TILE_32x256, TILE_64x128, TILE_96x256 = 0, 1, 2, 3, 4
+TILE_128x128, TILE_64x256, TILE_32x256, TILE_64x128 = 0, 1, 2, 3
 WDT_F32, WDT_BF16, WDT_F16, WDT_F32S, WDT_F32P = 0, 1, 2, 3, 4
-TILE_ROWS = {TILE_128x128: 128, TILE_64x256: 64, TILE_32x256: 32, TILE_64x128: 64,
-             TILE_96x256: 96}
+TILE_ROWS = {TILE_128x128: 128, TILE_64x256: 64, TILE_32x256: 32, TILE_64x128: 64}
 DT_F32, DT_F16, DT_BF16, DT_I32 = 0, 1, 2, 3
 
 

@@ -171,7 +171,7 @@ struct ConvGroup {
 // half the bytes of the fp32-I/O kernel; accumulation stays fp32.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int WT, bool V4, bool IO16 = false,
           bool GA = false>
-__global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P || BM == 96) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
+__global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ? 2 : 3) void conv1d_mfma_kernel(const ConvGroup G) {
   static_assert(!IO16 || WT != VITS_WDT_F32, "IO16 needs a 16-bit operand type");
   const int gi = (int)blockIdx.z / G.batch;
   const vits_conv1d_desc& p = G.d[gi];
@@ -1292,10 +1292,8 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
     if (e.tile != d.tile || e.epi != d.epi || (e.split < e.m) != (d.split < d.m) ||
         e.wdtype != d.wdtype)
       return VITS_E_UNSUP;
-    const int bm = d.tile == VITS_TILE_128x128 ? 128 : d.tile == VITS_TILE_32x256 ? 32
-                 : d.tile == VITS_TILE_96x256 ? 96 : 64;
-    const int bn = d.tile == VITS_TILE_64x256 || d.tile == VITS_TILE_32x256 ||
-                   d.tile == VITS_TILE_96x256 ? 256 : 128;
+    const int bm = d.tile == VITS_TILE_128x128 ? 128 : d.tile == VITS_TILE_32x256 ? 32 : 64;
+    const int bn = d.tile == VITS_TILE_64x256 || d.tile == VITS_TILE_32x256 ? 256 : 128;
     blocks += (long)((e.n_out + bn - 1) / bn) * ((e.m + bm - 1) / bm) * g.batch;
   }
   switch (d.tile) {
@@ -1328,13 +1326,6 @@ int conv1d_dispatch(const ConvGroup& g, hipStream_t s) {
     }
     case VITS_TILE_32x256:
       return launch_tile<32, 256, 1, 4, WT, GA>(g, s);
-    case VITS_TILE_96x256:
-      // 96-row layers (the wave discriminators' 96-channel convs): one
-      // 96-row block instead of two 64-row blocks with a quarter of padding
-      // rows; 4 waves of 96 x 64 (three A and two B fragments per k-step)
-      if constexpr (BF && WT != VITS_WDT_F32S && WT != VITS_WDT_F32P && !GA)
-        return launch_tile<96, 256, 1, 4, WT, GA>(g, s);
-      return VITS_E_UNSUP;
     default:
       return VITS_E_UNSUP;
   }

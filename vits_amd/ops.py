@@ -20,8 +20,7 @@ import torch
 from . import _lib
 from ._lib import (ACT_NONE, WDT_BF16, WDT_F16, WDT_F32, WDT_F32P, WDT_F32S, ConvDesc, ConvOut, EPI_GATE, EPI_STORE,
                    ResblockPairDesc,
-                   EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_96x256,
-                   TILE_ROWS,
+                   EPI_UPSAMPLE, TILE_128x128, TILE_32x256, TILE_64x128, TILE_64x256, TILE_ROWS,
                    check)
 
 # ---------------------------------------------------------------------------
@@ -107,8 +106,7 @@ def _pick_tile_bf16(m: int, k: int) -> int:
     return TILE_64x128
 
 
-TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, TILE_64x128: 128,
-             TILE_96x256: 256}
+TILE_COLS = {TILE_128x128: 128, TILE_64x256: 256, TILE_32x256: 256, TILE_64x128: 128}
 W_TILE_FLOATS = 4096                                   # conv1d.hip VITS_W_TILE
 X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::floats
 
@@ -117,8 +115,7 @@ X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::
 # conv1d.hip: 128x128 154 VGPRs -> 3 waves/SIMD, 64x256 / 32x256 ~122 -> 4,
 # 64x128 89 -> 5; 64x256 is budgeted at 3: its k=7 convs run faster with the
 # bigger chunk); the K-chunk is sized so that LDS does not cut this further
-TILE_OCCUPANCY = {TILE_128x128: 3, TILE_64x256: 3, TILE_32x256: 4, TILE_64x128: 5,
-                  TILE_96x256: 2}
+TILE_OCCUPANCY = {TILE_128x128: 3, TILE_64x256: 3, TILE_32x256: 4, TILE_64x128: 5}
 # experiment knob (tools/ab_*.sh): VITS_TILE_OCC="tile:wgs,..." overrides entries
 for _kv in filter(None, os.environ.get("VITS_TILE_OCC", "").split(",")):
     _t, _o = _kv.split(":")

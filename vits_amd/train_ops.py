@@ -41,8 +41,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from ._lib import (EPI_GATE, EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_96x256,
-                   TILE_128x128,
+from ._lib import (EPI_GATE, EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128,
                    WDT_BF16, WDT_F16, WDT_F32, ConvWgradDesc, check)
 from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
                   layer_norm_channels, layer_norm_channels_backward, make_desc, make_out,
@@ -61,9 +60,6 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
     k7: 307 -> 377 TF/s)."""
     if m > 32 and n_out is not None and n_out <= 128:
         return TILE_128x128 if (m >= 128 and k <= 5) else TILE_64x128
-    if m == 96 and TILE96 and k > 1 and (n_out is None or n_out >= 1024):
-        # the wave discriminators' 96-channel convs: one 96-row block
-        return TILE_96x256
     if 64 < m <= 128 and 3 < k <= 7:
         return TILE_64x128
     return _pick_tile_bf16(m, k)
@@ -75,11 +71,8 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
 # MFMA k-step per chunk and waits on every chunk's loads.
 TRAIN_KCK = int(os.environ.get("VITS_TRAIN_KCK", "64"))
 _GA_ALL = os.environ.get("VITS_GA16") == "2"  # weights from global memory: no W LDS budget
-_TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32,
-            TILE_96x256: 96}
-_TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256,
-            TILE_96x256: 256}
-TILE96 = os.environ.get("VITS_TILE96", "1") != "0"  # A/B switch
+_TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32}
+_TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256}
 
 
 def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
