@@ -459,17 +459,49 @@ __device__ void stft_fwd2_block(const StftJobD& J, int fblk, int b, float* sm) {
   float* const ws = xs + seglen;
   const int woff = (n - J.win) / 2;
   const float* xb = J.x + (int64_t)b * J.L;
-  for (int m = threadIdx.x; m < n; m += STFT_WG) {
-    const int h = m < n / 2 ? m : m - n / 2;
-    const float c = g_tw.c[h * (FFT_MAX / n)], sn = g_tw.s[h * (FFT_MAX / n)];
-    twc[m] = m < n / 2 ? c : -c;
-    tws[m] = m < n / 2 ? sn : -sn;
-    const int wi = m - woff;
-    ws[m] = (wi >= 0 && wi < J.win) ? J.window[wi] : 0.f;
+  // staging in groups of UNR elements per thread whose loads are all issued
+  // (from clamped addresses, zeroed after) before the first LDS write: a
+  // conditional load per element is a branch with its own wait, one memory
+  // round trip per element
+  constexpr int UNR = 8;
+  for (int m0 = threadIdx.x; m0 < n; m0 += STFT_WG * UNR) {
+    float c[UNR], sn[UNR], wv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int m = m0 + u * STFT_WG;
+      const int mm = m < n ? m : 0;
+      const int h = mm < n / 2 ? mm : mm - n / 2;
+      const int wi = mm - woff;
+      c[u] = g_tw.c[h * (FFT_MAX / n)];
+      sn[u] = g_tw.s[h * (FFT_MAX / n)];
+      wv[u] = J.window[(wi >= 0 && wi < J.win) ? wi : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int m = m0 + u * STFT_WG;
+      if (m < n) {
+        const int wi = m - woff;
+        twc[m] = m < n / 2 ? c[u] : -c[u];
+        tws[m] = m < n / 2 ? sn[u] : -sn[u];
+        ws[m] = (wi >= 0 && wi < J.win) ? wv[u] : 0.f;
+      }
+    }
   }
-  for (int i = threadIdx.x; i < seglen; i += STFT_WG) {
-    const int t = seg0 + i;
-    xs[i] = (t >= -J.pad && t < J.L + J.pad) ? xb[reflect_idx(t, J.L)] : 0.f;
+  for (int i0 = threadIdx.x; i0 < seglen; i0 += STFT_WG * UNR) {
+    float v[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int i = i0 + u * STFT_WG;
+      const int t = seg0 + i;
+      const bool ok = i < seglen && t >= -J.pad && t < J.L + J.pad;
+      v[u] = xb[ok ? reflect_idx(t, J.L) : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int i = i0 + u * STFT_WG;
+      const int t = seg0 + i;
+      if (i < seglen) xs[i] = (t >= -J.pad && t < J.L + J.pad) ? v[u] : 0.f;
+    }
   }
   __syncthreads();
   const int it = threadIdx.x;
