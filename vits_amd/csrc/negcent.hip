@@ -105,16 +105,12 @@ __global__ __launch_bounds__(256) void neg_cent_kernel2(const float* __restrict_
     constexpr int G = 8;
     for (int d0 = tid >> 5; d0 < C; d0 += 8 * G) {
       float lv[G], mv[G];
-      // (unconditional loads from a clamped address, zeroed after: a
-      // conditional load is a branch with its own wait per row)
 #pragma unroll
       for (int i = 0; i < G; ++i) {
         const int d = d0 + 8 * i;
         const bool ok = d < C && x < Ts;
-        const int64_t o = ok ? (int64_t)d * Ts + x : 0;
-        const float l = lb[o], mm = mb[o];
-        lv[i] = ok ? l : 0.f;
-        mv[i] = ok ? mm : 0.f;
+        lv[i] = ok ? lb[(int64_t)d * Ts + x] : 0.f;
+        mv[i] = ok ? mb[(int64_t)d * Ts + x] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < G; ++i) {
@@ -160,10 +156,8 @@ __global__ __launch_bounds__(256) void neg_cent_kernel2(const float* __restrict_
 #pragma unroll
     for (int i = 0; i < NC_PF; ++i) {
       const int d = 2 * (p0 + i) + lhi;
-      const int64_t o = d < C ? (int64_t)d * Tt : 0;  // (za / zbb: clamped rows)
-      const float va = za[o], vb = zbb[o];
-      zna[i] = (yva && d < C) ? va : 0.f;
-      znb[i] = (yvb && d < C) ? vb : 0.f;
+      zna[i] = (yva && d < C) ? za[(int64_t)d * Tt] : 0.f;
+      znb[i] = (yvb && d < C) ? zbb[(int64_t)d * Tt] : 0.f;
     }
   };
   zload(0);
