@@ -45,8 +45,10 @@ def main():
     lib = _lib.load()
     for name, B, cin, cout, k, dil, pad, T, slope in SHAPES:
         n_out = T + 2 * pad - (k - 1) * dil
-        x = torch.randn(B, cin, T, device=dev)
-        dy = torch.randn(B, cout, n_out, device=dev)
+        io16 = os.environ.get("IO16", "0") == "1"  # the training step's fp16 activations
+        dt = torch.float16 if io16 else torch.float32
+        x = torch.randn(B, cin, T, device=dev, dtype=dt)
+        dy = torch.randn(B, cout, n_out, device=dev, dtype=dt)
         flops = 2.0 * B * cout * cin * k * n_out
 
         def desc(dw, db, cpw=0):
@@ -56,6 +58,7 @@ def main():
             d.tin, d.n_out, d.k, d.dil, d.pad_left = T, n_out, k, dil, pad
             d.in_slope = slope
             d.dw_t, d.dbias, d.wdtype, d.reserved = dw.data_ptr(), db.data_ptr(), TRAIN_WDTYPE, cpw
+            d.io16 = int(io16)
             return d
 
         dw_t = torch.zeros(k, cout, cin, device=dev)
