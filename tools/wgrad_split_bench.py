@@ -43,7 +43,10 @@ def timeit(fn, n=20):
 def main():
     dev = torch.device("cuda:0")
     lib = _lib.load()
+    only = os.environ.get("ONLY")  # one shape name (PMC passes: tools/pmc_wgrad.sh)
     for name, B, cin, cout, k, dil, pad, T, slope in SHAPES:
+        if only and name != only:
+            continue
         n_out = T + 2 * pad - (k - 1) * dil
         io16 = os.environ.get("IO16", "0") == "1"  # the training step's fp16 activations
         dt = torch.float16 if io16 else torch.float32
