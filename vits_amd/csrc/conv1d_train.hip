@@ -249,7 +249,45 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
     }
   };
   auto lstore_vec = [&](uint16_t* st) {
-    if constexpr (IO16) unpack_io16();
+    if constexpr (IO16) {
+      // raw 16-bit blocks: dY as one 8-byte store per unit, X channel pairs
+      // interleaved bitwise when no prologue runs - the same bits as the
+      // float round trip below (exact for 16-bit values) in a quarter of the
+      // VALU work (the kernel is VALU-issue-bound)
+      typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = tid + 256 * q;
+        if (do_bias)
+          bsum[q] += ((float)dyr[q][0] + (float)dyr[q][1]) + ((float)dyr[q][2] + (float)dyr[q][3]);
+        *reinterpret_cast<t16x4*>(st + (u >> 4) * DY_LD + 4 * (u & 15)) = dyr[q];
+      }
+      uint32_t* xl = reinterpret_cast<uint32_t*>(st + DY_HALVES);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = tid + 256 * q;
+        const int cl = 2 * (u >> 5);
+        const int r4 = 4 * (u & 31);
+        if (r4 < wr + sh) {
+          if (!act_in) {
+            const u16x4 a = __builtin_bit_cast(u16x4, xr[2 * q]);
+            const u16x4 b = __builtin_bit_cast(u16x4, xr[2 * q + 1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              xl[((r4 + i) * X_LD + cl) >> 1] = (uint32_t)a[i] | ((uint32_t)b[i] << 16);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              float v0 = (float)xr[2 * q][i], v1 = (float)xr[2 * q + 1][i];
+              v0 = v0 < 0.f ? v0 * slope : v0;
+              v1 = v1 < 0.f ? v1 * slope : v1;
+              xl[((r4 + i) * X_LD + cl) >> 1] = pack2<WT>(v0, v1);
+            }
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int u = tid + 256 * q;
