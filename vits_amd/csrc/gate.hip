@@ -36,7 +36,11 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const E* __restrict__ x, 
   }
 }
 
-template <typename E>
+// V4: rows 4-element aligned (T % 4 == 0, strides and bases aligned): one
+// 4-element load / store per row and thread - the element-wise map issued a
+// 2-byte access per lane (half-width transactions) and left most of a
+// T = 500 row's threads idle after two iterations
+template <typename E, bool V4 = false>
 __global__ __launch_bounds__(256) void gate_bwd_kernel(const E* __restrict__ dy, int64_t dy_bs,
                                                       int dy_cs, const E* __restrict__ x,
                                                       int64_t x_bs, int x_cs,
@@ -55,6 +59,27 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const E* __restrict__ dy,
   const float ga = g ? (float)g[(int64_t)b * g_bs + p] : 0.f;
   const float gb = g ? (float)g[(int64_t)b * g_bs + H + p] : 0.f;
   float sa = 0.f, sb = 0.f;
+  if constexpr (V4) {
+    typedef E e4 __attribute__((ext_vector_type(4)));
+    for (int t = 4 * threadIdx.x; t < T; t += 1024) {
+      const e4 xav = *reinterpret_cast<const e4*>(xa + t);
+      const e4 xbv = *reinterpret_cast<const e4*>(xb + t);
+      const e4 dv = *reinterpret_cast<const e4*>(dyr + t);
+      e4 dav, dbv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float a = tanhf((float)xav[i] + ga);
+        const float s = sigm((float)xbv[i] + gb);
+        const float d = (float)dv[i];
+        dav[i] = (E)(d * s * (1.0f - a * a));
+        dbv[i] = (E)(d * a * s * (1.0f - s));
+        sa += (float)dav[i];
+        sb += (float)dbv[i];
+      }
+      *reinterpret_cast<e4*>(dxa + t) = dav;
+      *reinterpret_cast<e4*>(dxb + t) = dbv;
+    }
+  } else
   for (int t = threadIdx.x; t < T; t += 256) {
     const float a = tanhf((float)xa[t] + ga);
     const float s = sigm((float)xb[t] + gb);
@@ -142,11 +167,22 @@ extern "C" int vits_gate_backward_io16(const void* dy, int64_t dy_bstride, int32
   VITS_CHECK_SHAPE(batch <= 65535);
   const dim3 grid(half_channels, batch);
   hipStream_t s = as_stream(stream);
+  const bool v4 = (t_len & 3) == 0 && ((dy_bstride | dy_cstride | x_bstride | x_cstride |
+                                        dx_bstride | dx_cstride | (int64_t)half_channels) & 3) == 0 &&
+                  ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) |
+                    reinterpret_cast<uintptr_t>(dx)) & 7) == 0;
 #define VITS_GATE_BWD(E)                                                                           \
-  hipLaunchKernelGGL(gate_bwd_kernel<E>, grid, dim3(256), 0, s, static_cast<const E*>(dy),        \
-                     dy_bstride, dy_cstride, static_cast<const E*>(x), x_bstride, x_cstride,      \
-                     static_cast<const E*>(g), g_bstride, static_cast<E*>(dx), dx_bstride,       \
-                     dx_cstride, dg, half_channels, t_len)
+  if (v4)                                                                                          \
+    hipLaunchKernelGGL((gate_bwd_kernel<E, true>), grid, dim3(256), 0, s,                         \
+                       static_cast<const E*>(dy), dy_bstride, dy_cstride,                          \
+                       static_cast<const E*>(x), x_bstride, x_cstride, static_cast<const E*>(g),   \
+                       g_bstride, static_cast<E*>(dx), dx_bstride, dx_cstride, dg, half_channels,  \
+                       t_len);                                                                     \
+  else                                                                                             \
+    hipLaunchKernelGGL(gate_bwd_kernel<E>, grid, dim3(256), 0, s, static_cast<const E*>(dy),      \
+                       dy_bstride, dy_cstride, static_cast<const E*>(x), x_bstride, x_cstride,    \
+                       static_cast<const E*>(g), g_bstride, static_cast<E*>(dx), dx_bstride,     \
+                       dx_cstride, dg, half_channels, t_len)
   if (wdtype == VITS_WDT_F16)
     VITS_GATE_BWD(_Float16);
   else if (wdtype == VITS_WDT_BF16)
