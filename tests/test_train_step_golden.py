@@ -300,7 +300,16 @@ def test_train_step_gpu_fp16_autocast_vs_reference(device, monkeypatch):
     print("HIP fp16 :", {k: f"{v:.2e}" for k, v in hip.items()})
     print("torch f16:", {k: f"{v:.2e}" for k, v in ref16.items()})
     for k in hip:
-        assert hip[k] <= 2.0 * ref16[k] + 1e-3, (k, hip[k], ref16[k])
+        ref = ref16[k]
+        if k in ("g_param_gnorm", "g_small_grad"):
+            # max over G's parameters: set by the chaotic late-decoder gains
+            # (dec.resblocks.8.conds.*.weight_g), whose fp16 gradient is noise
+            # (relative error >= 1 for torch's own autocast step too: 0.43 /
+            # 1.9 and 1.6 / 2.6 on two runs) - those are checked as a
+            # distribution, the stable parameters one by one, in
+            # test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast
+            ref = max(ref, 1.0)
+        assert hip[k] <= 2.0 * ref + 1e-3, (k, hip[k], ref16[k])
 
 
 @pytest.mark.gpu
@@ -323,9 +332,12 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
     whose wgrad split-K sums are not ordered).  So:
 
     * every parameter the perturbation leaves in place (cos(t16', t16) >=
-      0.99, at least half of them - all discriminator, encoder and flow
-      layers): cos(HIP, t16) >= 0.99 and |log(|HIP| / |t16|)| <= 0.05 + 3
-      |log(|t16'| / |t16|)|;
+      0.999, at least half of them - all discriminator, encoder and flow
+      layers): 1 - cos(HIP, t16) <= max(0.01, 3 (1 - cos(t16', t16))) and
+      |log(|HIP| / |t16|)| <= 0.05 + 3 |log(|t16'| / |t16|)|.  (With a 0.99
+      stability line, late-decoder gains / cond biases at cos(t16', t16)
+      0.990-0.994 counted as stable and failed at random: cos(HIP, t16)
+      0.88-0.99 from run to run);
     * the chaotic rest, as a distribution: the median cos(HIP, t16) no lower
       than the median cos(t16', t16) - 0.1 (a wrong decoder kernel moves the
       whole distribution, rounding noise moves single parameters).
@@ -350,9 +362,9 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
     bad, stable, ch_c, cp_c = [], 0, [], []
     for k, (ch, rh) in hip_t16.items():
         cp, rp = pp_t16[k]
-        if cp >= 0.99:
+        if cp >= 0.999:
             stable += 1
-            if ch < 0.99 or abs(np.log(rh)) > 0.05 + 3 * abs(np.log(rp)):
+            if ch < 1.0 - max(0.01, 3 * (1.0 - cp)) or abs(np.log(rh)) > 0.05 + 3 * abs(np.log(rp)):
                 bad.append((k, ch, cp, rh, rp))
         else:
             ch_c.append(ch)
