@@ -35,7 +35,6 @@
  *                            (stft_loss.py:47-95) in one launch
  *   vits_layer_norm_channels modules.LayerNorm (modules.py:41-44)
  *   vits_attention_forward   MultiHeadAttention.attention core
- *   vits_attention_train_*   the same under autograd (dropout; backward)
  *                            (attentions.py:85-100)
  */
 #ifndef VITS_AMD_H
@@ -152,27 +151,6 @@ typedef struct vits_conv1d_desc {
   /* bucket; consumers never read past lengths[b] + halo, halo < len_skip,  */
   /* and [lengths[b], lengths[b] + len_skip) is written as zeros); 0 = off  */
   int32_t len_skip;
-  /* row-joined 2-D convs (the STFT discriminators' Conv2d(C, O, (k0, k1),   */
-  /* stride (s0, 1), padding (0, p1)), mrd.py:122-133, as a 1-D conv over   */
-  /* frequency rows laid end to end in padded rows of L columns: [B][C][F] */
-  /* [L], L = T + 2 p1 rounded up to 4, zeros in each row's pad columns).    */
-  /* x_rowlen = L > 0: window column n of x is read at (n / L) * x_rowmul + */
-  /* n % L (x_rowmul = s0 * L: output row f reads input rows s0 f + i);     */
-  /* x_cgroup > 0: virtual channel v = i * x_cgroup + c (frequency tap i,    */
-  /* real channel c) is read at c * x_cstride + i * x_gstride (a K-chunk    */
-  /* must not straddle two taps when x_cgroup >= kc).  y_rowlen = L > 0:    */
-  /* output column n is written at (n / L) * y_rowmul + n % L, and as 0     */
-  /* where n % L lies outside [y_rowpad, y_rowpad + y_rowvalid) (the pad   */
-  /* columns the next layer reads as its zero padding); gmask / res use    */
-  /* the output's column map.  All 0 = plain 1-D conv.                      */
-  int32_t x_rowlen;
-  int32_t x_rowmul;
-  int32_t x_cgroup;
-  int32_t x_gstride;
-  int32_t y_rowlen;
-  int32_t y_rowmul;
-  int32_t y_rowpad;
-  int32_t y_rowvalid;
 } vits_conv1d_desc;
 
 #define VITS_WDT_F32 0
@@ -235,9 +213,11 @@ int vits_expand_prior(const float* attn, const float* m, const float* s, const f
 /*   the device exactly as numpy's legacy RandomState does (masked         */
 /*   rejection) from noise_start = [B][VITS_ED_DRAWS] raw MT19937 uint32    */
 /*   words; lens must then have n_stage + 1 rows: lens[n_stage][b] = words  */
-/*   consumed (the host re-advances its generator by that many), or -1 when */
-/*   the slice does not fit (the reference's randint raises; z = 0, no     */
-/*   noise read).  t_x <= 4096, n_stage <= 8.                               */
+/*   consumed (the host re-advances its generator by that many), -1 when   */
+/*   the slice does not fit (the reference's randint raises), -2 when all  */
+/*   VITS_ED_DRAWS words were rejected (the host advances by the pool and  */
+/*   calls again with the next words); z = 0 and no noise read for both.  */
+/*   t_x <= 4096, n_stage <= 8.                                             */
 #define VITS_ED_DRAWS 32
 /* ---------------------------------------------------------------------- */
 int vits_expand_durations(const float* logw, int64_t logw_bstride, const int32_t* x_len, int t_x,
@@ -357,15 +337,6 @@ int vits_layer_norm_channels(const float* x, const float* r, const float* gamma,
                              int64_t post_add_bstride, float scale, const float* pos,
                              const float* pos_alpha, void* stream);
 
-/* backward of y = LN(x) * gamma + beta (training; gamma optional):        */
-/*   dx [B][C][T]; dgamma_part / dbeta_part (optional) [B * ceil(T/64)][C] */
-/*   per-tile partial sums the caller reduces over rows.                   */
-/*   Replaces the autograd of modules.LayerNorm (modules.py:41-44).        */
-int vits_layer_norm_channels_backward(const float* x, const float* gamma, const float* dy,
-                                      float* dx, float* dgamma_part, float* dbeta_part,
-                                      int batch, int channels, int t_len, float eps,
-                                      void* stream);
-
 /* ---------------------------------------------------------------------- */
 /* scaled-dot-product attention over [B][H*D][T] channel-major q/k/v      */
 /* (batch stride qkv_bstride, e.g. slices of one fused q|k|v buffer), key */
@@ -376,28 +347,6 @@ int vits_attention_forward(const float* q, const float* k, const float* v, float
                            int batch, int heads, int head_dim, int t_len,
                            int64_t qkv_bstride, int64_t out_bstride, const int32_t* lengths,
                            void* stream);
-
-/* ---------------------------------------------------------------------- */
-/* Training attention (MultiHeadAttention.attention, attentions.py:85-100, */
-/* under autograd with p_dropout): q/k/v/out contiguous [B][H*D][T] of     */
-/* dtype VITS_WDT_F16 (the fp16 projection convs' outputs) or _F32, fp32   */
-/* MFMA arithmetic; mask from lengths (scores.masked_fill(-1e4) of the      */
-/* x_mask outer product); keep [B][H][T][T] uint8 (NULL: no dropout)        */
-/* scales the probabilities by keep * keep_scale as nn.Dropout does.       */
-/* The forward writes lse [B][H][T][2] (fp32 row max m and 1 / row sum per */
-/* query) for the backward, which recomputes P = exp(S - m) / l and writes */
-/* dq, dk, dv (same layout/dtype);                                          */
-/* delta [B][H][T] fp32 is its scratch.  head_dim in {32, 64, 96, 128}.    */
-/* ---------------------------------------------------------------------- */
-int vits_attention_train_forward(const void* q, const void* k, const void* v,
-                                 const uint8_t* keep, float keep_scale, void* out, float* lse,
-                                 int batch, int heads, int head_dim, int t_len,
-                                 const int32_t* lengths, int dtype, void* stream);
-int vits_attention_train_backward(const void* q, const void* k, const void* v, const void* out,
-                                  const void* dout, const uint8_t* keep, float keep_scale,
-                                  const float* lse, float* delta, void* dq, void* dk, void* dv,
-                                  int batch, int heads, int head_dim, int t_len,
-                                  const int32_t* lengths, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------- */
 /* Training-step convs (backward of every stride-1 nn.Conv1d the          */
@@ -456,19 +405,14 @@ typedef struct vits_conv1d_wgrad_desc {
   float in_slope;         /* forward's leaky-relu prologue slope (1 = none)  */
   float* dw_t;            /* += dW as [k][cout][cin] fp32 (caller zeroes)    */
   float* dbias;           /* += sum_{b,t} dY [cout] fp32, or NULL            */
-  int32_t wdtype;         /* MFMA operand type: VITS_WDT_F16 / VITS_WDT_BF16 */
+  int32_t wdtype;         /* MFMA operand type: VITS_WDT_F16 / VITS_WDT_BF16, */
+                          /* or VITS_WDT_F32 (fp32 dy / x, exact-fp32 MFMA,  */
+                          /* split mode only; the fp32 training step)        */
   int32_t reserved;       /* > 0: (b, t)-chunks of 64 steps per workgroup    */
                           /* (tuning override), 0 = automatic                */
   int32_t io16;           /* dy / x are tensors of the 16-bit operand type   */
                           /* (strides in elements)                           */
   int32_t reserved2;
-  /* row-joined 2-D layers (see vits_conv1d_desc.x_rowlen): x column t at */
-  /* (t / x_rowlen) * x_rowmul + t % x_rowlen, virtual channel v = i *     */
-  /* x_cgroup + c at c * x_cstride + i * x_gstride; dy plain; 0 = off      */
-  int32_t x_rowlen;
-  int32_t x_rowmul;
-  int32_t x_cgroup;
-  int32_t x_gstride;
 } vits_conv1d_wgrad_desc;
 /* dW[co][ci][j] = sum_{b,t} dY[b][co][t] * act(x[b][ci][t - pad_left + j*dil]) */
 /* (operands rounded to wdtype, fp32 accumulation; VITS_E_UNSUP when       */
@@ -671,6 +615,23 @@ int vits_wn_update_backward(const float* gx, const void* gx16, const float* gout
 /* library introspection */
 const char* vits_amd_version(void);
 int vits_amd_device_arch(char* buf, int len);
+
+/* Dispatch counters: how many kernel launches each family of entry points */
+/* has issued since the last reset (host-side counts, one per launched     */
+/* kernel, incremented only when the launch was accepted).  Tests use them */
+/* to prove that a step ran on this library's kernels (not a torch path).  */
+#define VITS_CNT_CONV_F32 0      /* vits_conv1d_forward*: exact fp32 MFMA    */
+#define VITS_CNT_CONV_SPLIT 1    /*   split fp32 (VITS_WDT_F32S / F32P)     */
+#define VITS_CNT_CONV_16 2       /*   bf16 / fp16 operands                  */
+#define VITS_CNT_WGRAD_F32 3     /* vits_conv1d_wgrad(_split), fp32 operands */
+#define VITS_CNT_WGRAD_16 4      /*   16-bit operands                       */
+#define VITS_CNT_GATE_F32 5      /* vits_gate_forward / _backward           */
+#define VITS_CNT_GATE_16 6       /* vits_gate_*_io16                        */
+#define VITS_CNT_RESBLOCK 7      /* vits_resblock_pair*_forward             */
+#define VITS_CNT_PACK 8          /* vits_conv1d_pack*                       */
+#define VITS_CNT_N 9
+int64_t vits_dispatch_count(int which);
+void vits_dispatch_count_reset(void);
 
 #ifdef __cplusplus
 }

@@ -27,6 +27,8 @@ def _load():
         lib = C.CDLL(_SO)
         lib.mas_oracle_maximum_path.restype = None
         lib.mas_oracle_maximum_path.argtypes = [C.c_void_p] * 4 + [C.c_int] * 3
+        lib.mas_oracle_maximum_path_mt.restype = None
+        lib.mas_oracle_maximum_path_mt.argtypes = [C.c_void_p] * 4 + [C.c_int] * 4
         _lib = lib
     return _lib
 
@@ -40,6 +42,19 @@ def maximum_path_lengths(neg_cent: np.ndarray, t_t: np.ndarray, t_s: np.ndarray)
     ts = np.ascontiguousarray(t_s, dtype=np.int32)
     _load().mas_oracle_maximum_path(path.ctypes.data, vals.ctypes.data, tt.ctypes.data,
                                     ts.ctypes.data, B, Tt, Ts)
+    return path
+
+
+def maximum_path_lengths_mt(neg_cent: np.ndarray, t_t: np.ndarray, t_s: np.ndarray,
+                            threads: int) -> np.ndarray:
+    """maximum_path_lengths with the batch over `threads` OpenMP threads."""
+    vals = np.ascontiguousarray(neg_cent, dtype=np.float32).copy()
+    B, Tt, Ts = vals.shape
+    path = np.empty((B, Tt, Ts), dtype=np.int32)
+    tt = np.ascontiguousarray(t_t, dtype=np.int32)
+    ts = np.ascontiguousarray(t_s, dtype=np.int32)
+    _load().mas_oracle_maximum_path_mt(path.ctypes.data, vals.ctypes.data, tt.ctypes.data,
+                                       ts.ctypes.data, B, Tt, Ts, int(threads))
     return path
 
 

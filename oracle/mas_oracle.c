@@ -68,3 +68,17 @@ void mas_oracle_maximum_path(int32_t* paths, float* values, const int32_t* t_ys,
                       t_xs[b], T_x);
   }
 }
+
+/* The same, the batch spread over `threads` OpenMP threads (one utterance's
+ * DP per task): the CPU baseline of the GPU MAS kernel in bench.py's
+ * kernels leg ("MAS CPU = the C++ restatement with OpenMP
+ * over batch").  Bitwise the serial result. */
+void mas_oracle_maximum_path_mt(int32_t* paths, float* values, const int32_t* t_ys,
+                                const int32_t* t_xs, int B, int T_y, int T_x, int threads) {
+  const size_t per = (size_t)T_y * T_x;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+  for (int b = 0; b < B; ++b) {
+    memset(paths + (size_t)b * per, 0, sizeof(int32_t) * per);
+    maximum_path_each(paths + (size_t)b * per, values + (size_t)b * per, t_ys[b], t_xs[b], T_x);
+  }
+}

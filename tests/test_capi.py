@@ -54,7 +54,7 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu
  offsetof(vits_resblock_pair_desc, post_div), sizeof(vits_wnorm_layer),
  sizeof(vits_snorm_layer), offsetof(vits_snorm_layer, eps), VITS_WNORM_MAX, VITS_SNORM_MAX,
  sizeof(vits_pack16_layer), offsetof(vits_pack16_layer, img_t), offsetof(vits_pack16_layer, cin_pad_t),
- offsetof(vits_conv1d_desc, x_rowlen), offsetof(vits_conv1d_desc, y_rowvalid));
+ offsetof(vits_conv1d_desc, gmask_slope), offsetof(vits_conv1d_desc, len_skip));
  return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -81,5 +81,19 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu
     assert int(out[15]) == ctypes.sizeof(Pack16Layer)
     assert int(out[16]) == Pack16Layer.img_t.offset
     assert int(out[17]) == Pack16Layer.cin_pad_t.offset
-    assert int(out[18]) == ConvDesc.x_rowlen.offset
-    assert int(out[19]) == ConvDesc.y_rowvalid.offset
+    assert int(out[18]) == ConvDesc.gmask_slope.offset
+    assert int(out[19]) == ConvDesc.len_skip.offset
+
+
+def test_dispatch_counters_host_side():
+    """vits_dispatch_count / _reset are plain host functions (no GPU): one
+    counter per VITS_CNT_* family of the header, reset to zero, -1 outside."""
+    from vits_amd import _lib
+
+    with open(os.path.join(ROOT, "include", "vits_amd.h")) as f:
+        n = int(re.search(r"#define VITS_CNT_N (\d+)", f.read()).group(1))
+    assert len(_lib.CNT_NAMES) == n
+    _lib.dispatch_counts_reset()
+    assert set(_lib.dispatch_counts().values()) == {0}
+    lib = _lib.load()
+    assert lib.vits_dispatch_count(-1) == -1 and lib.vits_dispatch_count(n) == -1

@@ -132,3 +132,31 @@ def test_build_spec_cache_gpu_matches_spectrogram(tmp_path, device):
     ref2 = _ref_spectrogram(load_wav_to_torch(ds.filepaths_sid[1][1])[0].unsqueeze(0))[0]
     assert (spec2 - ref2).abs().max().item() / ref2.abs().max().item() < 1e-4
     assert os.path.exists(_spec_filename(ds.filepaths_sid[1][1]))
+
+
+def test_wav_header_any_pcm_width(tmp_path):
+    """build_spec_cache's header pass (data_utils._wav_header): sample rate
+    and sample count for 16-bit / float WAVs and for 24-bit PCM, which
+    scipy's memory-mapped read refuses."""
+    import struct
+
+    import numpy as np
+    from scipy.io import wavfile
+
+    from vits_amd.data_utils import _wav_header
+
+    p = tmp_path / "a.wav"
+    wavfile.write(p, 16000, (np.arange(12345) % 300).astype(np.int16))
+    assert _wav_header(str(p)) == (16000, 12345)
+    p = tmp_path / "b.wav"
+    wavfile.write(p, 22050, np.zeros(777, np.float32))
+    assert _wav_header(str(p)) == (22050, 777)
+    n = 1001
+    data = b"".join(struct.pack("<i", i * 100)[:3] for i in range(n)) + b"\0"
+    fmt = struct.pack("<HHIIHH", 1, 1, 16000, 16000 * 3, 3, 24)
+    riff = (b"RIFF" + struct.pack("<I", 4 + 8 + len(fmt) + 8 + len(data)) + b"WAVE" + b"fmt "
+            + struct.pack("<I", len(fmt)) + fmt + b"LIST" + struct.pack("<I", 3) + b"abc\0"
+            + b"data" + struct.pack("<I", 3 * n) + data)
+    p = tmp_path / "c.wav"
+    p.write_bytes(riff)
+    assert _wav_header(str(p)) == (16000, n)

@@ -20,7 +20,9 @@ Paths:
   swapped for their CPU checkers (MAS: oracle/mas_oracle.c, neg_cent:
   oracle/vits_oracle.py, STFT magnitude: torch.stft).
 * GPU fp32 (fp16_run off): HIP MAS, neg_cent, STFT magnitude + adjoint,
-  weight / spectral norms, FusedRAdam; convs are torch's.
+  weight / spectral norms, FusedRAdam, and every generator / wave-
+  discriminator conv and gate on the fp32 HIP training kernels (the STFT
+  discriminators' Conv2d layers stay MIOpen's).
 * GPU fp16 autocast (fp16_run on, configs/base.json's setting): every
   generator / wave-discriminator conv and gate on the HIP training kernels
   with fp16 activations; the GradScaler's initial scale is 1024 so the
@@ -130,7 +132,31 @@ def _run_step(G, cfg, device, fp16, perturb=0.0):
     """One step on the golden inputs; returns (step, outputs, G params
     before, D params before) with the gradients left on the parameters.
     perturb: every parameter element scaled by (1 +- perturb), random signs
-    (seeded), before the step."""
+    (seeded), before the step.
+
+    MIOpen runs its deterministic solvers here (torch.backends.cudnn.
+    deterministic): with its default find, the STFT discriminators' Conv2d
+    layers (the only MIOpen convs of the step) pick solvers whose results
+    differ from run to run - tools/determinism.py traced every run-to-run
+    difference of the HIP fp16 step to d.mfd.*.convs.3 (the first MIOpen
+    layer), and with deterministic solvers two HIP steps are bit-identical
+    in every forward output, backward gradient and parameter gradient
+    (profiles/r05_determinism.txt)."""
+    with _deterministic_miopen():
+        return _run_step_(G, cfg, device, fp16, perturb)
+
+
+class _deterministic_miopen:
+    def __enter__(self):
+        self._old = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+
+    def __exit__(self, *exc):
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = self._old
+        return False
+
+
+def _run_step_(G, cfg, device, fp16, perturb):
     st = _make_step(cfg, device, fp16)
     if perturb:
         gen = torch.Generator().manual_seed(123)
@@ -178,7 +204,7 @@ def grad_agreement(ga, gb, gref, rel_floor=1e-3):
     return res
 
 
-def _metrics(G, cfg, device, fp16):
+def _metrics(G, cfg, device, fp16, exclude=()):
     """Run the step once; return {metric: max relative error} vs the golden.
 
     Per-parameter metrics skip gradients below 1e-6 of the total gradient
@@ -187,7 +213,9 @@ def _metrics(G, cfg, device, fp16):
     noise).  Updates are compared in aggregate, sum over parameters of
     |sum(update) - ref| / sum of |ref update| (AdamW's first step moves
     every weight by +-lr, so this is the fraction of weights whose update
-    sign disagrees), since single near-zero gradient elements may flip."""
+    sign disagrees), since single near-zero gradient elements may flip.
+    exclude: "g.name" / "d.name" parameters left out of the per-parameter
+    metrics (param_gnorm, small_grad)."""
     st, out, g0, d0 = _run_step(G, cfg, device, fp16)
     rep = {}
     for k in ("loss_disc", "loss_gen", "loss_stft", "loss_dur", "loss_kl", "loss_kl_q",
@@ -204,7 +232,7 @@ def _metrics(G, cfg, device, fp16):
         e_g, num_u, den_u = 0.0, 0.0, 0.0
         for k, (gn, gs, dsum, dabs) in zip(keys, G[pre + "stats"]):
             p = params[k]
-            if gn > floor:
+            if gn > floor and pre[0] + "." + k not in exclude:
                 g = p.grad.detach().double().cpu()
                 e_g = max(e_g, abs(g.norm().item() - gn) / gn)
             delta = (p.detach().double() - before[k].double()).cpu()
@@ -217,7 +245,7 @@ def _metrics(G, cfg, device, fp16):
             g = params[str(k)].grad.detach().float().cpu().numpy().ravel()
             ref = G[pre + "small_grad"][off:off + g.size]
             off += g.size
-            if np.linalg.norm(ref) > floor:
+            if np.linalg.norm(ref) > floor and pre[0] + "." + str(k) not in exclude:
                 e = float(np.abs(g - ref).max() / np.abs(ref).max())
                 if e > e_s:
                     e_s, worst = e, str(k)
@@ -273,8 +301,43 @@ def test_train_step_cpu_fp32_vs_reference(monkeypatch):
 
 @pytest.mark.gpu
 def test_train_step_gpu_fp32_vs_reference(device):
+    """fp32 training (fp16_run: false) on the GPU: every generator and wave-
+    discriminator Conv1d / ConvTranspose1d and every WN / ResBlock2 gate runs
+    on this library's fp32 training kernels (Conv1dHip32 / ConvGateHip32:
+    the split- / exact-fp32 conv for forward and input gradient, the exact-
+    fp32 MFMA weight-gradient kernel, the fp32 gate backward), so the fp32
+    bars below pin those kernels' backward across the whole step, the late
+    decoder included.  The dispatch counters prove they ran."""
+    from vits_amd import _lib
+
     G, cfg = _load()
+    _lib.dispatch_counts_reset()
     _run_and_check(G, cfg, device, False, FP32_TOL)
+    c = _lib.dispatch_counts()
+    print("dispatches:", c)
+    assert c["conv_split"] > 0 and c["conv_f32"] > 0, c
+    assert c["wgrad_f32"] > 0 and c["gate_f32"] > 0, c
+    assert c["conv_16"] == 0 and c["wgrad_16"] == 0 and c["gate_16"] == 0, c
+
+
+def _chaotic(G, cfg, device, monkeypatch, line=0.999):
+    """Parameters whose fp16 gradient is chaotic on this step: cos(t16',
+    t16) < line, t16' = the reference's fp16 autocast step with every
+    parameter scaled by (1 +- 2^-11) (one fp16 rounding), t16 = the same step
+    unperturbed.  Returns (names, g_t16, g_pp)."""
+    from vits_amd import discriminators, train_ops
+
+    with monkeypatch.context() as mp:
+        mp.setattr(train_ops, "HIP_TRAIN", False)
+        mp.setattr(discriminators, "STFT_D_HIP", False)
+        st, *_ = _run_step(G, cfg, device, True)
+        g_t16 = _grads(st)
+        st, *_ = _run_step(G, cfg, device, True, perturb=2.0 ** -11)
+        g_pp = _grads(st)
+    # every parameter the per-parameter metrics look at (their floor is 1e-6
+    # of the network's gradient norm), small ones included
+    pp = grad_agreement(g_pp, g_t16, g_t16, rel_floor=1e-6)
+    return {k for k, (c, _) in pp.items() if c < line}, g_t16, g_pp
 
 
 @pytest.mark.gpu
@@ -285,31 +348,32 @@ def test_train_step_gpu_fp16_autocast_vs_reference(device, monkeypatch):
     GPU: the same step with every conv / gate on torch's autocast path
     (MIOpen fp16, exactly what train_stft.py runs) is measured against the
     same fp32 golden, and each HIP metric must be within 2x of it (plus a
-    1e-3 floor).  Measured on MI355X: aggregate update-sign disagreement
-    HIP 1.7e-2 vs torch-autocast 2.6e-2; worst per-parameter gradient norm
-    1.3 vs 1.9 (late-stage decoder gains / cond biases, sums with heavy
-    cancellation)."""
+    1e-3 floor).
+
+    The per-parameter maxima (param_gnorm, small_grad) leave out the
+    parameters whose fp16 gradient is chaotic on this random-init step
+    (_chaotic: the late-decoder gains / cond biases, whose gradients follow
+    fp16 rounding noise through the MR-STFT log magnitudes - relative error
+    ~1 for torch's own autocast step); they are checked as a distribution in
+    test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast."""
     from vits_amd import discriminators, train_ops
 
     G, cfg = _load()
-    hip = _metrics(G, cfg, device, True)
+    chaotic, _, _ = _chaotic(G, cfg, device, monkeypatch)
+    n_g = len(G["g_keys"])
+    n_gc = sum(1 for k in chaotic if k.startswith("g."))
+    print(f"{len(chaotic)} chaotic parameters ({n_gc} of G's {n_g}) left out of the "
+          "per-parameter maxima:", sorted(chaotic)[:12], "...")
+    assert n_gc <= n_g // 2 and not any(k.startswith("d.") for k in chaotic), sorted(chaotic)
+    hip = _metrics(G, cfg, device, True, exclude=chaotic)
     with monkeypatch.context() as mp:
-        mp.setattr(train_ops, "autocast_wdtype", lambda *a, **k: None)
+        mp.setattr(train_ops, "HIP_TRAIN", False)
         mp.setattr(discriminators, "STFT_D_HIP", False)
-        ref16 = _metrics(G, cfg, device, True)
+        ref16 = _metrics(G, cfg, device, True, exclude=chaotic)
     print("HIP fp16 :", {k: f"{v:.2e}" for k, v in hip.items()})
     print("torch f16:", {k: f"{v:.2e}" for k, v in ref16.items()})
     for k in hip:
-        ref = ref16[k]
-        if k in ("g_param_gnorm", "g_small_grad"):
-            # max over G's parameters: set by the chaotic late-decoder gains
-            # (dec.resblocks.8.conds.*.weight_g), whose fp16 gradient is noise
-            # (relative error >= 1 for torch's own autocast step too: 0.43 /
-            # 1.9 and 1.6 / 2.6 on two runs) - those are checked as a
-            # distribution, the stable parameters one by one, in
-            # test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast
-            ref = max(ref, 1.0)
-        assert hip[k] <= 2.0 * ref + 1e-3, (k, hip[k], ref16[k])
+        assert hip[k] <= 2.0 * ref16[k] + 1e-3, (k, hip[k], ref16[k])
 
 
 @pytest.mark.gpu
@@ -328,8 +392,8 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
     differentiate as 1 / |X| there, so the late decoder's gradients follow
     the rounding noise (measured on MI355X with tools/grad_noise.py: ~280 of
     ~500 parameters keep cosine >= 0.999 under the perturbation, ~150 fall
-    below 0.9, some to 0.35; the chaotic ones also move between two HIP runs,
-    whose wgrad split-K sums are not ordered).  So:
+    below 0.9, some to 0.35).  Two HIP runs are bit-identical here (MIOpen
+    on its deterministic solvers, _run_step).  So:
 
     * every parameter the perturbation leaves in place (cos(t16', t16) >=
       0.999, at least half of them - all discriminator, encoder and flow
@@ -348,14 +412,8 @@ def test_train_step_gpu_fp16_per_parameter_gradients_vs_torch_autocast(device, m
     G, cfg = _load()
     st, *_ = _run_step(G, cfg, device, True)
     g_hip = _grads(st)
-    with monkeypatch.context() as mp:
-        mp.setattr(train_ops, "autocast_wdtype", lambda *a, **k: None)
-        mp.setattr(discriminators, "STFT_D_HIP", False)
-        st, *_ = _run_step(G, cfg, device, True)
-        g_t16 = _grads(st)
-        st, *_ = _run_step(G, cfg, device, True, perturb=2.0 ** -11)
-        g_pp = _grads(st)
     del st
+    _, g_t16, g_pp = _chaotic(G, cfg, device, monkeypatch)
     assert set(g_hip) == set(g_t16) == set(g_pp)
     hip_t16 = grad_agreement(g_hip, g_t16, g_t16)
     pp_t16 = grad_agreement(g_pp, g_t16, g_t16)

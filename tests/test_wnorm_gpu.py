@@ -152,6 +152,23 @@ def _rel_l2(a, b):
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
+def _within_noise(ga, gb, gns, mult=3.0):
+    """Every parameter gradient of the fused path (ga) within mult x the hook
+    path's own noise envelope (the worst of its perturbed runs gns, each a
+    1-ulp weight perturbation) of the hook path (gb), plus 1e-3.  weight_g
+    (<dW_row, v_row> / ||v_row||, which cancels over the row: condition ~
+    sqrt(fan-in)) is held apart from the other parameters, each against its
+    own group's envelope; several perturbation draws (not one) set the
+    envelope, so a single noisy draw does not decide the bar."""
+    def worst(pairs, want_g):
+        return max(_rel_l2(a, b) for (n, a), (_, b) in pairs if n.endswith("weight_g") == want_g)
+
+    for want_g in (False, True):
+        fused = worst(zip(ga, gb), want_g)
+        floor = max(worst(zip(gn, gb), want_g) for gn in gns)
+        assert fused <= mult * floor + 1e-3, (want_g, fused, floor)
+
+
 def test_train_step_fused_spectral_norm_matches_torch_hooks():
     """One train_stft step (tiny config, fp16 autocast) with the one-launch
     spectral norm vs torch's hooks from identical models, batch and RNG
@@ -160,20 +177,25 @@ def test_train_step_fused_spectral_norm_matches_torch_hooks():
     parameter as close as the hook path is to itself when the D weights are
     perturbed by one fp32 ulp (W / sigma agrees to fp32 rounding; an element
     that rounds to the other fp16 neighbour in an autocast conv moves the
-    fp16 gradients, measured here as the noise floor; fused within 3x)."""
+    fp16 gradients, measured here as the noise floor over three perturbation
+    draws; fused within 3x, weight_g included)."""
     from test_train import _batch, _make, tiny_hps
 
     hps = tiny_hps()
     batch = [t.to(DEV) for t in _batch(hps, 4, seed=0)]
     res = []
     flags = wnorm.FUSED_NORMS, wnorm.FUSED_WN
+    old_det = torch.backends.cudnn.deterministic
     try:
         wnorm.FUSED_WN = False
-        for fused, perturb in ((True, False), (False, False), (False, True)):
+        # MIOpen's deterministic solvers: its default find makes the STFT
+        # discriminators' Conv2d layers differ from run to run
+        torch.backends.cudnn.deterministic = True
+        for fused, perturb in ((True, 0), (False, 0), (False, 11), (False, 12), (False, 13)):
             wnorm.FUSED_NORMS = fused
             st = _make(hps, DEV, seed=0)
             if perturb:
-                gen = torch.Generator(device=DEV).manual_seed(11)
+                gen = torch.Generator(device=DEV).manual_seed(perturb)
                 with torch.no_grad():
                     for n, p in st.net_d.named_parameters():
                         if n.endswith("weight_orig"):
@@ -189,22 +211,12 @@ def test_train_step_fused_spectral_norm_matches_torch_hooks():
             res.append((out, grads, [b.detach().clone() for b in st.net_d.buffers()]))
     finally:
         wnorm.FUSED_NORMS, wnorm.FUSED_WN = flags
-    (oa, ga, ba), (ob, gb, bb), (_, gn, _) = res
+        torch.backends.cudnn.deterministic = old_det
+    (oa, ga, ba), (ob, gb, bb) = res[:2]
     for k in ("loss_disc", "loss_gen_all", "loss_stft"):
         _close(oa[k], ob[k], 1e-3, k)
-    assert len(ga) == len(gb) == len(gn) and len(ga) > 100
-    # weight_g's gradient <dW_row, v_row> / ||v_row|| cancels over the row
-    # (condition ~ sqrt(fan-in), 20-30 here): rounding-level changes of dW
-    # move it by percents - measured on MI355X, switching the fused gate on
-    # moves it 2.6 % on the hook path and 16 % on the fused-norm path, a
-    # draw of that noise - so it gets its own, looser bar
-    def worst(pairs, want_g):
-        return max(_rel_l2(a, b) for (n, a), (_, b) in pairs if n.endswith("weight_g") == want_g)
-
-    for want_g, mult in ((False, 3.0), (True, 10.0)):
-        fused = worst(zip(ga, gb), want_g)
-        floor = worst(zip(gn, gb), want_g)
-        assert fused <= mult * floor + 1e-3, (want_g, fused, floor)
+    assert all(len(r[1]) == len(ga) for r in res) and len(ga) > 100
+    _within_noise(ga, gb, [r[1] for r in res[2:]])
     for i, (a, b) in enumerate(zip(ba, bb)):
         _close(a, b, 2e-3, f"D buffer {i}")
 
@@ -220,7 +232,7 @@ def test_generator_fused_weight_norm_matches_torch_hooks():
     round to the other fp16 neighbour in some autocast convs, and the fp16
     gate / conv chain carries that through; the noise floor is measured here
     by running the hook path with weight_g scaled by (1 + 2^-23 r), r ~ N(0,1),
-    and the fused path must stay within 3x of it.  (The train_stft losses
+    three draws, and the fused path must stay within 3x of the worst.  (The train_stft losses
     are not a usable probe: the MR-STFT log-magnitude term's gradient is
     discontinuous in y_hat.)"""
     from test_train import _batch, _make, tiny_hps
@@ -233,10 +245,10 @@ def test_generator_fused_weight_norm_matches_torch_hooks():
     res = []
     flag = wnorm.FUSED_WN
     try:
-        for fused, perturb in ((True, False), (False, False), (False, True)):
+        for fused, perturb in ((True, 0), (False, 0), (False, 11), (False, 12), (False, 13)):
             wnorm.FUSED_WN = fused
             with torch.no_grad():
-                gen = torch.Generator(device=DEV).manual_seed(11)
+                gen = torch.Generator(device=DEV).manual_seed(perturb or 11)
                 for p, p0 in zip(gs, g0):
                     p.copy_(p0 * (1 + 2.0 ** -23 * torch.randn(p.shape, device=DEV,
                                                                 generator=gen))
@@ -257,18 +269,41 @@ def test_generator_fused_weight_norm_matches_torch_hooks():
         with torch.no_grad():
             for p, p0 in zip(gs, g0):
                 p.copy_(p0)
-    (ya, ga), (yb, gb), (yn, gn) = res
+    (ya, ga), (yb, gb) = res[:2]
     _close(ya, yb, 2e-3, "y_hat")
-    assert len(ga) == len(gb) == len(gn) and len(ga) > 50
-    # weight_g's gradient <dW_row, v_row> / ||v_row|| cancels over the row
-    # (condition ~ sqrt(fan-in), 20-30 here): rounding-level changes of dW
-    # move it by percents - measured on MI355X, switching the fused gate on
-    # moves it 2.6 % on the hook path and 16 % on the fused-norm path, a
-    # draw of that noise - so it gets its own, looser bar
-    def worst(pairs, want_g):
-        return max(_rel_l2(a, b) for (n, a), (_, b) in pairs if n.endswith("weight_g") == want_g)
+    assert all(len(r[1]) == len(ga) for r in res) and len(ga) > 50
+    _within_noise(ga, gb, [r[1] for r in res[2:]])
 
-    for want_g, mult in ((False, 3.0), (True, 10.0)):
-        fused = worst(zip(ga, gb), want_g)
-        floor = worst(zip(gn, gb), want_g)
-        assert fused <= mult * floor + 1e-3, (want_g, fused, floor)
+
+def test_generator_fused_weight_norm_fp32_step():
+    """The same comparison in fp32 training (autocast off: every generator
+    conv on the fp32 HIP training kernels): no fp16 rounding to amplify, so
+    fused and hook paths must agree to fp32 summation order - y_hat to 1e-5
+    of its magnitude, every gradient (weight_g included) to 1e-3 relative."""
+    from test_train import _batch, _make, tiny_hps
+
+    hps = tiny_hps()
+    x, x_len, spec, spec_len, _, _, emo, spk = [t.to(DEV) for t in _batch(hps, 4, seed=0)]
+    st = _make(hps, DEV, seed=0)
+    res = []
+    flag = wnorm.FUSED_WN
+    try:
+        for fused in (True, False):
+            wnorm.FUSED_WN = fused
+            st.net_g.zero_grad(set_to_none=True)
+            torch.manual_seed(5)
+            with st._g_weights():
+                y_hat = st.net_g(x, x_len, spec, spec_len, emo, spk)[0]
+            cot = torch.randn(y_hat.shape, device=DEV,
+                              generator=torch.Generator(device=DEV).manual_seed(7))
+            (y_hat * cot).sum().backward()
+            torch.cuda.synchronize()
+            res.append((y_hat.detach(), [(n, p.grad.detach().clone())
+                                         for n, p in st.net_g.named_parameters()
+                                         if p.grad is not None]))
+    finally:
+        wnorm.FUSED_WN = flag
+    (ya, ga), (yb, gb) = res
+    _close(ya, yb, 1e-5, "y_hat")
+    worst = max(((_rel_l2(a, b), n) for (n, a), (_, b) in zip(ga, gb)))
+    assert worst[0] <= 1e-3, worst

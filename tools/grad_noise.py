@@ -24,9 +24,9 @@ def run(scale, hip, perturb=0.0):
         return st
 
     T._make_step = mk
-    aw, sd = train_ops.autocast_wdtype, discriminators.STFT_D_HIP
+    aw, sd = train_ops.HIP_TRAIN, discriminators.STFT_D_HIP
     if not hip:
-        train_ops.autocast_wdtype = lambda *a, **k: None
+        train_ops.HIP_TRAIN = False
         discriminators.STFT_D_HIP = False
     try:
         st = T._make_step(cfg, dev, True)
@@ -43,7 +43,7 @@ def run(scale, hip, perturb=0.0):
         ok = float(st.scaler.get_scale()) == scale
         return T._grads(st), ok
     finally:
-        train_ops.autocast_wdtype, discriminators.STFT_D_HIP = aw, sd
+        train_ops.HIP_TRAIN, discriminators.STFT_D_HIP = aw, sd
         T._make_step = orig
 
 
@@ -52,14 +52,12 @@ scale = 1024.0
 t16, ok1 = run(scale, False)
 tp, ok2 = run(scale, False, 2.0 ** -11)
 pp = T.grad_agreement(tp, t16, t16)
-for variant in ("default", "GATE_FUSED=0", "ATTN_HIP=0"):
-    saved = train_ops.GATE_FUSED, train_ops.ATTN_HIP
+for variant in ("default", "GATE_FUSED=0"):
+    saved = train_ops.GATE_FUSED
     if variant == "GATE_FUSED=0":
         train_ops.GATE_FUSED = False
-    if variant == "ATTN_HIP=0":
-        train_ops.ATTN_HIP = False
     h16, ok3 = run(scale, True)
-    train_ops.GATE_FUSED, train_ops.ATTN_HIP = saved
+    train_ops.GATE_FUSED = saved
     ht = T.grad_agreement(h16, t16, t16)
     print(f"--- HIP {variant}", flush=True)
     cp = np.array([pp[k][0] for k in pp])

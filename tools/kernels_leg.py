@@ -1,5 +1,5 @@
 """bench.kernels_leg alone (MAS, neg_cent, MR-STFT magnitudes) - for A/B
-runs of the training-side kernels (e.g. VITS_STFT_FWD=0 / 1)."""
+runs of the training-side kernels."""
 import json
 import os
 import sys

@@ -35,7 +35,7 @@ with torch.no_grad():
         m32 = bench.build_model(dev)
         ref = m32.infer_p2(*inputs).float()
         snr = 10 * torch.log10((ref ** 2).sum() / ((out - ref) ** 2).sum().clamp_min(1e-30))
-        print(f"snr vs fp32 {float(snr):.2f} dB (VITS_ACT16={os.environ.get('VITS_ACT16', '1')})")
+        print(f"snr vs fp32 {float(snr):.2f} dB")
 tot = sum(r["ms_per_step"] for r in rows)
 print(f"conv total {tot:.3f} ms/step over {len(rows)} shapes")
 for r in rows:

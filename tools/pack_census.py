@@ -1,15 +1,18 @@
 """Which convs still pack their 16-bit weight images per call (not served by
 train_ops.prepacked): one eager train_stft step (B=32, base config, fp16
-autocast) with VITS_PACK_TRACE=1, the per-call packs counted by call site.
-    VITS_PACK_TRACE=1 python tools/pack_census.py"""
+autocast) with train_ops.PACK_TRACE on, the per-call packs counted by call
+site.    python tools/pack_census.py"""
 import os
 import sys
 
-os.environ.setdefault("VITS_PACK_TRACE", "1")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
+import collections  # noqa: E402
+
 from vits_amd import train_ops  # noqa: E402
+
+train_ops.PACK_TRACE = collections.Counter()
 from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch  # noqa: E402
 
 dev = torch.device("cuda:0")

@@ -1,6 +1,6 @@
 """Which side moves in test_generator_fused_weight_norm_matches_torch_hooks
 with the fused gate: per-parameter rel. L2 of (fused WN vs hooks) with
-VITS_GATE_FUSED on / off, and the dtype torch._weight_norm returns under
+train_ops.GATE_FUSED on / off, and the dtype torch._weight_norm returns under
 fp16 autocast.   python tools/wn_gate_probe.py"""
 import os
 import sys

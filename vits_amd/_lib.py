@@ -81,14 +81,6 @@ class ConvDesc(C.Structure):
         ("gmask_slope", C.c_float),
         ("io16", C.c_int32),
         ("len_skip", C.c_int32),
-        ("x_rowlen", C.c_int32),
-        ("x_rowmul", C.c_int32),
-        ("x_cgroup", C.c_int32),
-        ("x_gstride", C.c_int32),
-        ("y_rowlen", C.c_int32),
-        ("y_rowmul", C.c_int32),
-        ("y_rowpad", C.c_int32),
-        ("y_rowvalid", C.c_int32),
     ]
 
 
@@ -167,10 +159,6 @@ class ConvWgradDesc(C.Structure):
         ("reserved", C.c_int32),
         ("io16", C.c_int32),
         ("reserved2", C.c_int32),
-        ("x_rowlen", C.c_int32),
-        ("x_rowmul", C.c_int32),
-        ("x_cgroup", C.c_int32),
-        ("x_gstride", C.c_int32),
     ]
 
 
@@ -304,23 +292,9 @@ _SIGS = {
         + [C.c_float, C.c_void_p, C.c_void_p, C.c_int64, C.c_float, C.c_void_p, C.c_void_p,
            C.c_void_p],
     ),
-    "vits_layer_norm_channels_backward": (
-        C.c_int,
-        [C.c_void_p] * 6 + [C.c_int] * 3 + [C.c_float, C.c_void_p],
-    ),
     "vits_attention_forward": (
         C.c_int,
         [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p],
-    ),
-    "vits_attention_train_forward": (
-        C.c_int,
-        [C.c_void_p] * 4 + [C.c_float] + [C.c_void_p] * 2 + [C.c_int] * 4
-        + [C.c_void_p, C.c_int, C.c_void_p],
-    ),
-    "vits_attention_train_backward": (
-        C.c_int,
-        [C.c_void_p] * 6 + [C.c_float] + [C.c_void_p] * 5 + [C.c_int] * 4
-        + [C.c_void_p, C.c_int, C.c_void_p],
     ),
     "vits_conv1d_pack16": (
         C.c_int,
@@ -388,6 +362,8 @@ _SIGS = {
         C.c_int, [C.c_void_p] * 6 + [C.c_int] * 4 + [C.c_void_p]),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
+    "vits_dispatch_count": (C.c_int64, [C.c_int]),
+    "vits_dispatch_count_reset": (None, []),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS.keys())
@@ -395,6 +371,21 @@ EXPORTED_SYMBOLS = tuple(_SIGS.keys())
 
 class VitsAmdError(RuntimeError):
     pass
+
+
+# vits_dispatch_count families (include/vits_amd.h VITS_CNT_*)
+CNT_NAMES = ("conv_f32", "conv_split", "conv_16", "wgrad_f32", "wgrad_16", "gate_f32",
+             "gate_16", "resblock", "pack")
+
+
+def dispatch_counts() -> dict:
+    """{family: kernel launches since the last reset} of the library."""
+    lib = load()
+    return {n: int(lib.vits_dispatch_count(i)) for i, n in enumerate(CNT_NAMES)}
+
+
+def dispatch_counts_reset() -> None:
+    load().vits_dispatch_count_reset()
 
 
 def lib_path() -> str:

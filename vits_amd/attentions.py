@@ -7,7 +7,6 @@ flash-style attention kernel, channel LayerNorm) via ``vits_amd.engine``.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 from torch import nn
@@ -19,7 +18,7 @@ from .modules import LayerNorm
 
 # self-attention's q / k / v projections as one HIP conv under autocast
 # (train_ops.conv1d_cat); VITS_QKV_CAT=0 keeps three
-QKV_CAT = os.environ.get("VITS_QKV_CAT", "1") != "0"
+QKV_CAT = True
 
 
 class MultiHeadAttention(nn.Module):
@@ -45,9 +44,9 @@ class MultiHeadAttention(nn.Module):
 
     def forward(self, x, c, attn_mask=None, lengths=None):
         """lengths (int [B], optional): the key / query lengths attn_mask was
-        built from (Encoder: x_mask outer product); with it, under autocast
-        on the GPU, the attention core runs on the HIP training kernels
-        (train_ops.AttentionHip: MFMA forward + backward, dropout fused)."""
+        built from (Encoder: x_mask outer product); unused in training, where
+        the attention core is the reference's batched matmul / softmax
+        (hipBLASLt; the inference plans run csrc/attention.hip instead)."""
         # 1x1 projections on the HIP training conv under autocast (torch otherwise)
         conv = train_ops.conv1d
         qkv = (train_ops.conv1d_cat((self.conv_q, self.conv_k, self.conv_v), x)
@@ -56,9 +55,7 @@ class MultiHeadAttention(nn.Module):
             q, k, v = qkv
         else:
             q, k, v = conv(self.conv_q, x), conv(self.conv_k, c), conv(self.conv_v, c)
-        y = train_ops.attention(q, k, v, self.n_heads, lengths, self.p_dropout, self.training)
-        if y is None:
-            y = self.attention(q, k, v, mask=attn_mask)[0]
+        y = self.attention(q, k, v, mask=attn_mask)[0]
         return conv(self.conv_o, y)
 
     def attention(self, query, key, value, mask=None):

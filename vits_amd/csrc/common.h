@@ -36,3 +36,10 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// host-side dispatch counters (vits_dispatch_count, include/vits_amd.h)
+void vits_count(int which, int n = 1);
+static inline int count_ok(int rc, int which, int n = 1) {
+  if (rc == VITS_OK) vits_count(which, n);
+  return rc;
+}

@@ -54,14 +54,6 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
   if (d.io16) VITS_CHECK_ARG(d.wdtype == VITS_WDT_BF16 || d.wdtype == VITS_WDT_F16);
   // row-joined 2-D layers: 4-column blocks within one row, single-output
   // STORE, K-chunks inside one frequency tap
-  VITS_CHECK_ARG(d.x_rowlen >= 0 && d.y_rowlen >= 0 && d.x_cgroup >= 0);
-  if (d.x_rowlen) VITS_CHECK_SHAPE((d.x_rowlen & 3) == 0 && d.x_rowmul >= d.x_rowlen &&
-                                   d.x_tstride == 1);
-  if (d.x_cgroup) VITS_CHECK_SHAPE(d.x_cgroup % d.kc == 0);
-  if (d.y_rowlen)
-    VITS_CHECK_ARG(d.epi == VITS_EPI_STORE && d.split >= d.m && d.y_rowmul >= d.y_rowlen &&
-                   d.y_rowpad >= 0 && d.y_rowvalid >= 0 &&
-                   d.y_rowpad + d.y_rowvalid <= d.y_rowlen);
   return VITS_OK;
 }
 
@@ -72,14 +64,8 @@ int check_desc(const vits_conv1d_desc& d, int batch) {
 // LDS-staged weights, and the fp16-I/O training convs (kc up to 64, io16 = 1)
 // lose ~3 % of the train step; the 16-bit-activation inference decoder
 // (io16 = 2) takes it for every group (C5, B=4 Ty=2500 bf16: conv time 12.9
-// -> 12.2 ms/step, its k=3 and 2-tap upsampler groups included).  VITS_GA16=0 / =2: never / always.
+// -> 12.2 ms/step, its k=3 and 2-tap upsampler groups included).
 bool ga16(const vits_conv1d_desc* d, int n) {
-  static const int mode = [] {
-    const char* e = getenv("VITS_GA16");
-    return e ? e[0] - '0' : 1;
-  }();
-  if (mode == 0) return false;
-  if (mode == 2) return true;
   int kmax = 0;
   for (int i = 0; i < n; ++i) {
     if (d[i].io16 == 1) return false;
@@ -98,18 +84,30 @@ int conv1d_group(const vits_conv1d_desc* d, int n, int batch, hipStream_t s) {
     if (rc) return rc;
     g.d[i] = d[i];
   }
+  int rc, which;
   switch (d[0].wdtype) {
     case VITS_WDT_BF16:
-      return ga16(d, n) ? vits_conv1d_dispatch_bf16g(g, s) : vits_conv1d_dispatch_bf16(g, s);
+      rc = ga16(d, n) ? vits_conv1d_dispatch_bf16g(g, s) : vits_conv1d_dispatch_bf16(g, s);
+      which = VITS_CNT_CONV_16;
+      break;
     case VITS_WDT_F16:
-      return ga16(d, n) ? vits_conv1d_dispatch_f16g(g, s) : vits_conv1d_dispatch_f16(g, s);
+      rc = ga16(d, n) ? vits_conv1d_dispatch_f16g(g, s) : vits_conv1d_dispatch_f16(g, s);
+      which = VITS_CNT_CONV_16;
+      break;
     case VITS_WDT_F32S:
-      return vits_conv1d_dispatch_f32s(g, s);
+      rc = vits_conv1d_dispatch_f32s(g, s);
+      which = VITS_CNT_CONV_SPLIT;
+      break;
     case VITS_WDT_F32P:
-      return vits_conv1d_dispatch_f32p(g, s);
+      rc = vits_conv1d_dispatch_f32p(g, s);
+      which = VITS_CNT_CONV_SPLIT;
+      break;
     default:
-      return vits_conv1d_dispatch_f32(g, s);
+      rc = vits_conv1d_dispatch_f32(g, s);
+      which = VITS_CNT_CONV_F32;
   }
+  if (rc == VITS_OK) vits_count(which);
+  return rc;
 }
 
 // a group that cannot share one grid (different tiles / epilogues / staging

@@ -295,17 +295,8 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   int xlds[T4 ? NU : 1];  // T4: the unit's LDS element offset ([t][kcp] image)
   const int nbq = (nb + 3) >> 2;
   const int nunits = T4 ? kc * nbq : V4 ? kc * nb : xsz;
-  // window column -> element offset in an x row (row-joined 2-D layers:
-  // column tt of output row tt / L reads input row s0 * (tt / L), see
-  // vits_conv1d_desc.x_rowlen; L % 4 == 0 keeps a 4-column block in one row)
-  const int xrl = p.x_rowlen;
-  auto xcol = [&](int tt) -> int {
-    if (xrl > 0) {
-      const int f = tt / xrl;
-      return f * p.x_rowmul + (tt - f * xrl);
-    }
-    return tt * (int)xts;
-  };
+  // window column -> element offset in an x row
+  auto xcol = [&](int tt) -> int { return tt * (int)xts; };
 #pragma unroll
   for (int q = 0; q < NU; ++q) {
     const int u = tid + q * 256;
@@ -407,16 +398,8 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   // unconditionally (padding lanes read the batch's first element) so the
   // compiler cannot tie a wait to each load: all MAXX loads stay in flight
   // under the chunk's MFMAs and are consumed in lstore.
-  // first row of K-chunk c0 (virtual channels of row-joined 2-D layers:
-  // v = i * x_cgroup + c at c * x_cstride + i * x_gstride; a chunk lies
-  // within one frequency tap i)
-  auto chunk_base = [&](int c0) -> int64_t {
-    if (p.x_cgroup > 0) {
-      const int i = c0 / p.x_cgroup;
-      return (int64_t)(c0 - i * p.x_cgroup) * p.x_cstride + (int64_t)i * p.x_gstride;
-    }
-    return (int64_t)c0 * p.x_cstride;
-  };
+  // first row of K-chunk c0
+  auto chunk_base = [&](int c0) -> int64_t { return (int64_t)c0 * p.x_cstride; };
   auto gload = [&](int c0) {
     const io_t* base = xb + chunk_base(c0);
     const int lim = p.cin - c0;  // rows >= lim are channel padding
@@ -1100,15 +1083,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
         // 32x32 sub-tile is issued before the first store, so the 16 round
         // trips overlap (res may alias y: each element is still read before
         // it is written, by the same lane).
-        // output column map of row-joined 2-D layers (vits_conv1d_desc.y_rowlen)
-        int ncol = n;
-        bool rmask = false;
-        if (p.y_rowlen > 0) {
-          const int f = n / p.y_rowlen;
-          const int tl = n - f * p.y_rowlen;
-          ncol = f * p.y_rowmul + tl;
-          rmask = tl < p.y_rowpad || tl >= p.y_rowpad + p.y_rowvalid;
-        }
+        const int ncol = n;
         if (n < p.n_out) {
           // (row blocks of RH: 8 would halve the temporaries of tiles with 8
           // live accumulator sub-tiles)
@@ -1157,7 +1132,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
 #pragma unroll
             for (int i = 0; i < RH; ++i) v[i] = yo[i] + v[i];
           }
-          const bool msk = n >= len_b || rmask;
+          const bool msk = n >= len_b;
 #pragma unroll
           for (int i = 0; i < RH; ++i) {
             const int r = r0 + i;
@@ -1191,9 +1166,7 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
       return VITS_E_UNSUP;
     if (WT == VITS_WDT_F32P && d.kc != 16 && d.kc != 32) return VITS_E_UNSUP;
     // 32-bit window offsets
-    const int64_t maxcol = d.x_rowlen > 0
-                               ? ((int64_t)(d.tin + BN) / d.x_rowlen + 1) * d.x_rowmul
-                               : (int64_t)(d.tin + BN) * d.x_tstride;
+    const int64_t maxcol = (int64_t)(d.tin + BN) * d.x_tstride;
     if ((int64_t)d.kc * d.x_cstride + maxcol >= (1LL << 31)) return VITS_E_UNSUP;
     if (V4 && (IO16 || SPL)) {  // T4 staging: kc/4 channel quads x ceil(nb/4)*4 blocks
       constexpr int nu = (XTile<BN, BF, IO16 || WT == VITS_WDT_F32P>::floats / 16 + 48 + 255) / 256;
@@ -1260,7 +1233,6 @@ int launch_tile(const ConvGroup& g, hipStream_t s) {
     const int align = d.io16 ? 7 : 15;
     const bool v4 = d.x_tstride == 1 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
                     (d.tin & 3) == 0 && d.pad_left >= 0 &&
-                    (d.x_rowlen == 0 || ((d.x_rowmul & 3) == 0 && (d.x_gstride & 3) == 0)) &&
                     (reinterpret_cast<uintptr_t>(d.x) & align) == 0 &&
                     (size_t)d.kc * xrs4[i] <=
                         (size_t)((d.io16 || WT == VITS_WDT_F32P) ? XTile<BN, BF, true>::floats

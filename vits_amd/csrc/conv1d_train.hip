@@ -132,22 +132,9 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
   // VEC window: rows from the 4-aligned start t0 - pad_left - sh
   const int sh = VEC ? ((p.pad_left & 3) ? 4 - (p.pad_left & 3) : 0) : 0;
 
-  // x addressing (row-joined 2-D layers, vits_conv1d_wgrad_desc.x_rowlen):
-  // virtual channel v -> row base, window column t -> offset in the row
-  auto vbase = [&](int v) -> int64_t {
-    if (p.x_cgroup > 0) {
-      const int i = v / p.x_cgroup;
-      return (int64_t)(v - i * p.x_cgroup) * p.x_cstride + (int64_t)i * p.x_gstride;
-    }
-    return (int64_t)v * p.x_cstride;
-  };
-  auto xcol = [&](int t) -> int {
-    if (p.x_rowlen > 0) {
-      const int f = t / p.x_rowlen;
-      return f * p.x_rowmul + (t - f * p.x_rowlen);
-    }
-    return t;
-  };
+  // x addressing: channel v -> row base, window column t -> offset in the row
+  auto vbase = [&](int v) -> int64_t { return (int64_t)v * p.x_cstride; };
+  auto xcol = [&](int t) -> int { return t; };
 
   typedef typename Op16<WT>::T T16;
   typedef T16 t16x4 __attribute__((ext_vector_type(4)));
@@ -487,6 +474,154 @@ __global__ __launch_bounds__(256, NK <= 5 ? 2 : 1) void wgrad_kernel(const vits_
   }
 }
 
+// ---- fp32 weight gradient (the fp32 training step, autocast off) ---------------
+// Same GEMM as wgrad_kernel (rows co, columns ci, one accumulator set per
+// tap, reduction over (b, t) split across workgroups into partial tiles) on
+// the exact-fp32 MFMA v_mfma_f32_32x32x2_f32: every product is an fp32
+// product, accumulated in fp32 (an fmaf chain per k-step pair), so the
+// result carries the reference's fp32 conv-backward precision.  Per chunk of
+// KT32 = 32 time steps the workgroup stages fp32
+//    dY[64 co][32 t]                 row-major, odd row stride (33)
+//    X~[32 + (k-1)*dil t][64 ci]     time-major, odd row stride (65)
+// both conflict-free for the staging stores (consecutive lanes: consecutive
+// t) and for the fragment reads (A: 32 rows of one column, B: 32 consecutive
+// ci of one row).  A k-step covers 2 time steps: A = dY[co][2s + lhi], B_j =
+// X~[2s + lhi + j*dil][ci].  Double-buffered (next chunk's loads in flight
+// under the current chunk's MFMAs), 67 KB of LDS: two workgroups per CU.
+constexpr int KT32 = 32;
+constexpr int MAX_WR32 = 96;                 // KT32 + (k-1)*dil <= 96
+constexpr int DY32_LD = KT32 + 1;
+constexpr int X32_LD = WG_N + 1;
+constexpr int DY32_FLOATS = WG_M * DY32_LD;
+constexpr int STAGE32 = DY32_FLOATS + MAX_WR32 * X32_LD;
+constexpr int NXQ32 = WG_N * MAX_WR32 / 256;  // staged X elements per thread (24)
+
+template <int NK>
+__global__ __launch_bounds__(256, 2) void wgrad_f32_kernel(const vits_conv1d_wgrad_desc p,
+                                                           int tchunks, int total_chunks,
+                                                           int chunks_per_wg,
+                                                           float* __restrict__ ws,
+                                                           float* __restrict__ ws_b) {
+  extern __shared__ __attribute__((aligned(16))) float lds32[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int l32 = lane & 31;
+  const int lhi = lane >> 5;
+  const int wm = (wid >> 1) * 32;
+  const int wn = (wid & 1) * 32;
+  const int m0 = blockIdx.z * WG_M;
+  const int c0 = blockIdx.y * WG_N;
+  const int ch_begin = blockIdx.x * chunks_per_wg;
+  const int ch_end = min(total_chunks, ch_begin + chunks_per_wg);
+  const int dil = p.dil;
+  const int wr = KT32 + (NK - 1) * dil;
+  const float slope = p.in_slope;
+  const bool act_in = slope != 1.0f;
+  const bool do_bias = p.dbias != nullptr && blockIdx.y == 0;
+
+  f32x16 acc[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  float bsum[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bsum[q] = 0.f;
+
+  // dY element (row (tid >> 5) + 8 q, column tid & 31); X element e = tid +
+  // 256 q -> (channel e / 96, window row e % 96)
+  const int dy_row0 = tid >> 5;
+  const int dy_col = tid & 31;
+  float dyv[8], xv[NXQ32];
+  auto gload = [&](int chunk) {
+    const int b = chunk / tchunks;
+    const int t0 = (chunk - b * tchunks) * KT32;
+    const float* dyb = p.dy + (int64_t)b * p.dy_bstride;
+    const int t = t0 + dy_col;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int co = m0 + dy_row0 + 8 * q;
+      dyv[q] = (co < p.cout && t < p.n_out) ? dyb[(int64_t)co * p.dy_cstride + t] : 0.f;
+    }
+    const float* xb = p.x + (int64_t)b * p.x_bstride;
+    const int ts = t0 - p.pad_left;
+#pragma unroll
+    for (int q = 0; q < NXQ32; ++q) {
+      const int e = tid + 256 * q;
+      const int cl = e / MAX_WR32;
+      const int r = e - cl * MAX_WR32;
+      const int tt = ts + r;
+      const bool ok = r < wr && tt >= 0 && tt < p.tin && c0 + cl < p.cin;
+      xv[q] = ok ? xb[(int64_t)(c0 + cl) * p.x_cstride + tt] : 0.f;
+    }
+  };
+  auto lstore = [&](float* st) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (do_bias) bsum[q] += dyv[q];
+      st[(dy_row0 + 8 * q) * DY32_LD + dy_col] = dyv[q];
+    }
+    float* xl = st + DY32_FLOATS;
+#pragma unroll
+    for (int q = 0; q < NXQ32; ++q) {
+      const int e = tid + 256 * q;
+      const int cl = e / MAX_WR32;
+      const int r = e - cl * MAX_WR32;
+      float v = xv[q];
+      if (act_in) v = v < 0.f ? v * slope : v;
+      if (r < wr) xl[r * X32_LD + cl] = v;
+    }
+  };
+
+  const int a_off = (wm + l32) * DY32_LD + lhi;
+  const int b_off = DY32_FLOATS + lhi * X32_LD + wn + l32;
+  if (ch_begin < ch_end) {
+    gload(ch_begin);
+    lstore(lds32);
+  }
+  __syncthreads();
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
+    const int it = ch - ch_begin;
+    float* cur = lds32 + (it & 1) * STAGE32;
+    float* nxt = lds32 + ((it + 1) & 1) * STAGE32;
+    const bool more = ch + 1 < ch_end;
+    if (more) gload(ch + 1);
+#pragma unroll
+    for (int s = 0; s < KT32 / 2; ++s) {
+      const float a = cur[a_off + 2 * s];
+#pragma unroll
+      for (int j = 0; j < NK; ++j) {
+        const float bv = cur[b_off + (2 * s + j * dil) * X32_LD];
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[j], 0, 0, 0);
+      }
+    }
+    if (more) lstore(nxt);
+    __syncthreads();
+  }
+
+  const int ci = c0 + wn + l32;
+  float* dst = ws + (int64_t)blockIdx.x * NK * p.cout * p.cin;
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = m0 + wm + 8 * (r >> 2) + 4 * lhi + (r & 3);
+      if (co < p.cout && ci < p.cin) dst[((int64_t)j * p.cout + co) * p.cin + ci] = acc[j][r];
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float v = bsum[q];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+      const int co = m0 + dy_row0 + 8 * q;
+      if ((tid & 31) == 0 && co < p.cout) ws_b[(int64_t)blockIdx.x * p.cout + co] = v;
+    }
+  }
+}
+
 // dw[co][ci][j] = sum_s ws[s][j][co][ci] (the parameter layout, written, not
 // accumulated: no zeroing), dbias[co] = sum_s ws_b[s][co].  A workgroup
 // reduces E = 256 / P consecutive slab elements with P lanes each over the
@@ -545,7 +680,8 @@ struct WgradSplit {
 };
 WgradSplit wgrad_split(const vits_conv1d_wgrad_desc& d, int batch, bool partial) {
   WgradSplit w;
-  w.tchunks = (d.n_out + KT - 1) / KT;
+  const int kt = d.wdtype == VITS_WDT_F32 ? KT32 : KT;
+  w.tchunks = (d.n_out + kt - 1) / kt;
   w.total = batch * w.tchunks;
   const int tiles = ((d.cout + WG_M - 1) / WG_M) * ((d.cin + WG_N - 1) / WG_N);
   if (!partial) {
@@ -569,6 +705,32 @@ WgradSplit wgrad_split(const vits_conv1d_wgrad_desc& d, int batch, bool partial)
   return w;
 }
 
+int wgrad_f32_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, float* ws,
+                       float* ws_b) {
+  const WgradSplit w = wgrad_split(d, batch, true);
+  dim3 grid(w.splits, (d.cin + WG_N - 1) / WG_N, (d.cout + WG_M - 1) / WG_M);
+  const size_t lds = 2 * STAGE32 * sizeof(float);
+  switch (d.k) {
+#define VITS_WG32_CASE(NK)                                                                         \
+  case NK:                                                                                         \
+    hipLaunchKernelGGL((wgrad_f32_kernel<NK>), grid, dim3(256), lds, s, d, w.tchunks, w.total,    \
+                       w.cpw, ws, ws_b);                                                           \
+    break;
+    VITS_WG32_CASE(1)
+    VITS_WG32_CASE(2)
+    VITS_WG32_CASE(3)
+    VITS_WG32_CASE(4)
+    VITS_WG32_CASE(5)
+    VITS_WG32_CASE(7)
+    VITS_WG32_CASE(9)
+    VITS_WG32_CASE(11)
+#undef VITS_WG32_CASE
+    default:
+      return VITS_E_UNSUP;
+  }
+  return vits_launch_status();
+}
+
 template <int WT, bool PARTIAL>
 int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, float* ws,
                    float* ws_b) {
@@ -582,8 +744,6 @@ int wgrad_dispatch(const vits_conv1d_wgrad_desc& d, int batch, hipStream_t s, fl
                    (reinterpret_cast<uintptr_t>(d.dy) & al) == 0 && (d.x_cstride & 3) == 0 &&
                    (d.x_bstride & 3) == 0 && (reinterpret_cast<uintptr_t>(d.x) & al) == 0 &&
                    (d.tin & 3) == 0 && KT + (d.k - 1) * d.dil + sh <= MAX_WR &&
-                   (d.x_rowlen == 0 ||
-                    ((d.x_rowlen & 3) == 0 && (d.x_rowmul & 3) == 0 && (d.x_gstride & 3) == 0)) &&
                    (d.k > 1 || d.io16);  // k = 1 (tools/wgrad_split_bench.py: 40 -> 53 us)
                                          // keeps the element-wise map for fp32 inputs
   switch (d.k) {
@@ -707,9 +867,11 @@ extern "C" int vits_conv1d_wgrad(const vits_conv1d_wgrad_desc* d, int batch, voi
   VITS_CHECK_SHAPE(d->n_out > 0 && d->tin > 0);
   if (KT + (d->k - 1) * d->dil > MAX_WR) return VITS_E_UNSUP;
   hipStream_t s = as_stream(stream);
-  if (d->wdtype == VITS_WDT_F16) return wgrad_dispatch<VITS_WDT_F16, false>(*d, batch, s, 0, 0);
-  if (d->wdtype == VITS_WDT_BF16) return wgrad_dispatch<VITS_WDT_BF16, false>(*d, batch, s, 0, 0);
-  return VITS_E_ARG;
+  if (d->wdtype == VITS_WDT_F16)
+    return count_ok(wgrad_dispatch<VITS_WDT_F16, false>(*d, batch, s, 0, 0), VITS_CNT_WGRAD_16);
+  if (d->wdtype == VITS_WDT_BF16)
+    return count_ok(wgrad_dispatch<VITS_WDT_BF16, false>(*d, batch, s, 0, 0), VITS_CNT_WGRAD_16);
+  return d->wdtype == VITS_WDT_F32 ? VITS_E_UNSUP : VITS_E_ARG;  // (fp32: split mode only)
 }
 
 extern "C" int64_t vits_conv1d_wgrad_workspace(const vits_conv1d_wgrad_desc* d, int batch) {
@@ -724,13 +886,19 @@ extern "C" int vits_conv1d_wgrad_split(const vits_conv1d_wgrad_desc* d, int batc
   VITS_CHECK_ARG(d->dy && d->x && d->dw_t && workspace);
   VITS_CHECK_ARG(batch > 0 && d->cout > 0 && d->cin > 0 && d->k > 0 && d->dil > 0);
   VITS_CHECK_SHAPE(d->n_out > 0 && d->tin > 0);
-  if (KT + (d->k - 1) * d->dil > MAX_WR) return VITS_E_UNSUP;
+  if (d->wdtype != VITS_WDT_F32 && KT + (d->k - 1) * d->dil > MAX_WR) return VITS_E_UNSUP;
   if (workspace_floats < vits_conv1d_wgrad_workspace(d, batch)) return VITS_E_ARG;
   const WgradSplit w = wgrad_split(*d, batch, true);
   float* ws_b = workspace + (int64_t)w.splits * d->k * d->cout * d->cin;
   hipStream_t s = as_stream(stream);
   int rc;
-  if (d->wdtype == VITS_WDT_F16)
+  const bool f32 = d->wdtype == VITS_WDT_F32;
+  if (f32) {
+    // fp32 operands: element-wise staging
+    if (d->io16) return VITS_E_UNSUP;
+    if (KT32 + (d->k - 1) * d->dil > MAX_WR32) return VITS_E_UNSUP;
+    rc = wgrad_f32_dispatch(*d, batch, s, workspace, ws_b);
+  } else if (d->wdtype == VITS_WDT_F16)
     rc = wgrad_dispatch<VITS_WDT_F16, true>(*d, batch, s, workspace, ws_b);
   else if (d->wdtype == VITS_WDT_BF16)
     rc = wgrad_dispatch<VITS_WDT_BF16, true>(*d, batch, s, workspace, ws_b);
@@ -760,7 +928,7 @@ extern "C" int vits_conv1d_wgrad_split(const vits_conv1d_wgrad_desc* d, int batc
     VITS_RED_CASE(64)
 #undef VITS_RED_CASE
   }
-  return vits_launch_status();
+  return count_ok(vits_launch_status(), f32 ? VITS_CNT_WGRAD_F32 : VITS_CNT_WGRAD_16, 2);
 }
 
 extern "C" int vits_conv1d_pack16_pair(const float* w, int cout, int cin, int k, void* out,
@@ -786,7 +954,7 @@ extern "C" int vits_conv1d_pack16_pair(const float* w, int cout, int cin, int k,
                        reinterpret_cast<__bf16*>(out_t), m_pad_t, (int)total_t);
   else
     return VITS_E_ARG;
-  return vits_launch_status();
+  return count_ok(vits_launch_status(), VITS_CNT_PACK);
 }
 
 extern "C" int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int transpose, void* out,
@@ -811,7 +979,7 @@ extern "C" int vits_conv1d_pack16(const float* w, int cout, int cin, int k, int 
                        transpose, reinterpret_cast<__bf16*>(out), m_pad, cin_pad, zero, zero_n);
   else
     return VITS_E_ARG;
-  return vits_launch_status();
+  return count_ok(vits_launch_status(), VITS_CNT_PACK);
 }
 
 extern "C" int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, int wdtype,
@@ -845,7 +1013,7 @@ extern "C" int vits_conv1d_pack16_pairs(const vits_pack16_layer* layers, int n, 
       hipLaunchKernelGGL(pack16_pairs_kernel<_Float16>, grid, dim3(256), 0, s, L);
     else
       hipLaunchKernelGGL(pack16_pairs_kernel<__bf16>, grid, dim3(256), 0, s, L);
-    const int rc = vits_launch_status();
+    const int rc = count_ok(vits_launch_status(), VITS_CNT_PACK);
     if (rc) return rc;
   }
   return VITS_OK;

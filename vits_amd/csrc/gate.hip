@@ -120,7 +120,7 @@ extern "C" int vits_gate_forward(const float* x, int64_t x_bstride, int32_t x_cs
   hipLaunchKernelGGL(gate_fwd_kernel<float>, dim3(half_channels, batch), dim3(256), 0, as_stream(stream),
                      x, x_bstride, x_cstride, g, g_bstride, y, y_bstride, y_cstride, half_channels,
                      t_len);
-  return vits_launch_status();
+  return count_ok(vits_launch_status(), VITS_CNT_GATE_F32);
 }
 
 extern "C" int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t dy_cstride,
@@ -133,7 +133,7 @@ extern "C" int vits_gate_backward(const float* dy, int64_t dy_bstride, int32_t d
   hipLaunchKernelGGL(gate_bwd_kernel<float>, dim3(half_channels, batch), dim3(256), 0, as_stream(stream),
                      dy, dy_bstride, dy_cstride, x, x_bstride, x_cstride, g, g_bstride, dx,
                      dx_bstride, dx_cstride, dg, half_channels, t_len);
-  return vits_launch_status();
+  return count_ok(vits_launch_status(), VITS_CNT_GATE_F32);
 }
 
 extern "C" int vits_gate_forward_io16(const void* x, int64_t x_bstride, int32_t x_cstride,
@@ -155,7 +155,7 @@ extern "C" int vits_gate_forward_io16(const void* x, int64_t x_bstride, int32_t 
   else
     return VITS_E_ARG;
 #undef VITS_GATE_FWD
-  return vits_launch_status();
+  return count_ok(vits_launch_status(), VITS_CNT_GATE_16);
 }
 
 extern "C" int vits_gate_backward_io16(const void* dy, int64_t dy_bstride, int32_t dy_cstride,
@@ -190,5 +190,5 @@ extern "C" int vits_gate_backward_io16(const void* dy, int64_t dy_bstride, int32
   else
     return VITS_E_ARG;
 #undef VITS_GATE_BWD
-  return vits_launch_status();
+  return count_ok(vits_launch_status(), VITS_CNT_GATE_16);
 }

@@ -227,8 +227,10 @@ __global__ __launch_bounds__(256) void expand_durations_kernel(
   // mask = the smallest 2^k - 1 >= rng (numpy's masked rejection for ranges
   // below 2^32).  The number of words consumed goes to lens[n_stage][b] so
   // the host re-advances its generator by exactly that many; -1 when the
-  // slice does not fit (the reference's randint raises) or the pool ran out:
-  // z is then all zeros and no noise element is read.
+  // slice does not fit (the reference's randint raises), -2 when every word
+  // of the pool was rejected (probability < 2^-32: the host advances by the
+  // whole pool and replays with the next words): z is then all zeros and no
+  // noise element is read.
   int64_t nbase = 0;
   bool noise_ok = true;
   if (noise_mode) {
@@ -239,6 +241,7 @@ __global__ __launch_bounds__(256) void expand_durations_kernel(
       if (rng == 0) {
         used = 0;
       } else {
+        used = -2;  // (until a word is accepted)
         uint32_t mask = rng;
         mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
         mask |= mask >> 8; mask |= mask >> 16;

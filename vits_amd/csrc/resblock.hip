@@ -414,9 +414,9 @@ extern "C" int vits_resblock_pair_forward(const vits_resblock_pair_desc* d, int 
   hipStream_t s = as_stream(stream);
   switch (d[0].channels) {
     case 32:
-      return rb_launch<32, 256, 1, 4>(g, s);
+      return count_ok(rb_launch<32, 256, 1, 4>(g, s), VITS_CNT_RESBLOCK);
     case 64:
-      return rb_launch<64, 256, 1, 4>(g, s);
+      return count_ok(rb_launch<64, 256, 1, 4>(g, s), VITS_CNT_RESBLOCK);
     default:
       return VITS_E_UNSUP;
   }

@@ -442,10 +442,10 @@ static int r16_run(const vits_resblock_pair_desc* d, int n, int batch, int wdtyp
 
 extern "C" int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch,
                                             int wdtype, void* stream) {
-  return r16_run(d, n, batch, wdtype, 0, stream);
+  return count_ok(r16_run(d, n, batch, wdtype, 0, stream), VITS_CNT_RESBLOCK);
 }
 
 extern "C" int vits_resblock_pair16_mean_forward(const vits_resblock_pair_desc* d, int n,
                                                  int batch, int wdtype, void* stream) {
-  return r16_run(d, n, batch, wdtype, 1, stream);
+  return count_ok(r16_run(d, n, batch, wdtype, 1, stream), VITS_CNT_RESBLOCK);
 }

@@ -683,16 +683,6 @@ __global__ __launch_bounds__(256) void stft_fwd2_multi_kernel(const StftJobs J) 
   stft_fwd2_any(J.job[j], local - b * J.per_b[j], b, sm2);
 }
 
-// same, register budget capped at 4 waves per SIMD (A/B: VITS_STFT_OCC=4)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void stft_fwd2_multi_kernel_o4(const StftJobs J) {
-  extern __shared__ float sm2[];
-  const int j = find_job(J, blockIdx.x);
-  const int local = blockIdx.x - (j ? J.end[j - 1] : 0);
-  const int b = local / J.per_b[j];
-  stft_fwd2_any(J.job[j], local - b * J.per_b[j], b, sm2);
-}
-
 __global__ __launch_bounds__(256) void stft_bwd_frames_kernel(const StftJobD J) {
   extern __shared__ float2 sfft[];
   stft_bwd_frames_block(J, blockIdx.x, blockIdx.y, sfft);
@@ -750,14 +740,10 @@ int make_job(StftJobD& J, const float* x, int batch, int length, const float* wi
 size_t job_lds(const StftJobD& J) { return sizeof(float2) * (2 * J.fpb * J.n + J.n / 2); }
 int job_fblocks(const StftJobD& J) { return (J.frames + J.fpb - 1) / J.fpb; }
 
-// forward kind: the two-pass register FFT for n = 128 .. 2048 (VITS_STFT_FWD=1,
-// default), the radix-4 Stockham LDS FFT otherwise / VITS_STFT_FWD=0 (A/B)
+// forward kind: the two-pass register FFT for n = 128 .. 2048, the radix-4
+// Stockham LDS FFT for other sizes
 bool use_fwd2(int n, int hop) {
-  static const bool on = [] {
-    const char* e = getenv("VITS_STFT_FWD");
-    return !e || e[0] != '0';
-  }();
-  return on && fwd2_frames(n) > 0 && hop <= n && fwd2_lds(n, hop) <= 64 * 1024;
+  return fwd2_frames(n) > 0 && hop <= n && fwd2_lds(n, hop) <= 64 * 1024;
 }
 int fwd2_fblocks(const StftJobD& J) {
   const int f = fwd2_frames(J.n);
@@ -845,14 +831,7 @@ extern "C" int vits_stft_mag_forward_multi(const vits_stft_job* jobs, int njobs,
   }
   hipStream_t s = as_stream(stream);
   if (M[0].njobs) {
-    static const bool o4 = [] {
-      const char* e = getenv("VITS_STFT_OCC");
-      return e && e[0] == '4';
-    }();
-    if (o4)
-      hipLaunchKernelGGL(stft_fwd2_multi_kernel_o4, dim3(blocks[0]), dim3(256), lds[0], s, M[0]);
-    else
-      hipLaunchKernelGGL(stft_fwd2_multi_kernel, dim3(blocks[0]), dim3(256), lds[0], s, M[0]);
+    hipLaunchKernelGGL(stft_fwd2_multi_kernel, dim3(blocks[0]), dim3(256), lds[0], s, M[0]);
     int rc = vits_launch_status();
     if (rc) return rc;
   }

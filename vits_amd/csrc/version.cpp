@@ -16,3 +16,22 @@ extern "C" int vits_amd_device_arch(char* buf, int len) {
   buf[len - 1] = 0;
   return VITS_OK;
 }
+
+#include <atomic>
+
+namespace {
+std::atomic<int64_t> g_counts[VITS_CNT_N];
+}
+
+void vits_count(int which, int n) {
+  if (which >= 0 && which < VITS_CNT_N) g_counts[which].fetch_add(n, std::memory_order_relaxed);
+}
+
+extern "C" int64_t vits_dispatch_count(int which) {
+  if (which < 0 || which >= VITS_CNT_N) return -1;
+  return g_counts[which].load(std::memory_order_relaxed);
+}
+
+extern "C" void vits_dispatch_count_reset(void) {
+  for (auto& c : g_counts) c.store(0, std::memory_order_relaxed);
+}

@@ -126,29 +126,61 @@ def _spectrogram(wavs, hp, device):
     return spec.cpu()
 
 
+def _wav_header(fn: str):
+    """(sample rate, sample count over all channels) of a RIFF/WAVE file from
+    its header alone: the 'fmt ' chunk's rate and bits per sample and the
+    'data' chunk's byte size (any PCM width - 24-bit included, which scipy's
+    memory-mapped read refuses - and WAVE_FORMAT_EXTENSIBLE).  Files the
+    parser does not recognise are read whole by scipy instead."""
+    import struct
+
+    try:
+        with open(fn, "rb") as f:
+            riff = f.read(12)
+            if len(riff) == 12 and riff[:4] in (b"RIFF", b"RIFX") and riff[8:12] == b"WAVE":
+                en = "<" if riff[:4] == b"RIFF" else ">"
+                sr = bits = None
+                while True:
+                    hdr = f.read(8)
+                    if len(hdr) < 8:
+                        break
+                    cid, size = hdr[:4], struct.unpack(en + "I", hdr[4:])[0]
+                    if cid == b"fmt ":
+                        fmt = f.read(size + (size & 1))
+                        sr = struct.unpack(en + "I", fmt[4:8])[0]
+                        bits = struct.unpack(en + "H", fmt[14:16])[0]
+                    elif cid == b"data" and sr is not None and bits:
+                        return int(sr), int(size // ((bits + 7) // 8))
+                    else:
+                        f.seek(size + (size & 1), 1)
+    except (OSError, struct.error):
+        pass
+    from scipy.io import wavfile
+
+    sr, data = wavfile.read(fn)
+    return int(sr), int(data.size)
+
+
 def build_spec_cache(filepaths_sid, hparams, device="cuda", overwrite=False, max_batch=64):
     """Write the ``.spec.pt`` cache of every utterance of a filelist that
     lacks one (``data_utils.py:73-81``), on the GPU.  Utterances of equal
     sample count share one batched HIP STFT launch (up to ``max_batch``).
     Each file holds the ``[F, T]`` float32 tensor the reference's
     ``torch.save(spec, ...)`` writes.  The first pass reads only each WAV's
-    header (sample rate, sample count; the data is memory-mapped, not
-    loaded); audio is loaded ``max_batch`` utterances at a time in the
+    header (sample rate, sample count: ``_wav_header``); audio is loaded ``max_batch`` utterances at a time in the
     compute loop, so host memory stays bounded by one batch whatever the
     dataset size.  Returns the number of files written."""
-    from scipy.io import wavfile
 
     hp = hparams.data
     todo: dict = {}
     for _vecfn, wavfn, _emofn, _sid in load_filepaths_and_sid(filepaths_sid):
         fn = _spec_filename(wavfn)
         if overwrite or not os.path.exists(fn):
-            sr, data = wavfile.read(wavfn, mmap=True)
+            sr, n = _wav_header(wavfn)
             if sr != hp.sampling_rate:
                 raise ValueError("{} {} SR doesn't match target {} SR".format(
                     wavfn, sr, hp.sampling_rate))
-            todo.setdefault(int(data.size), []).append((fn, wavfn))
-            del data
+            todo.setdefault(n, []).append((fn, wavfn))
     written = 0
     for _n, items in sorted(todo.items()):
         for i in range(0, len(items), max_batch):

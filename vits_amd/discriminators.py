@@ -10,7 +10,6 @@ MultiWaveSTFTDiscriminator 200-236.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -109,47 +108,14 @@ class STFTDiscriminator(nn.Module):
         h = x.unsqueeze(1)
         layers = list(self.convs)
         first = layers[0]
-        wdt = train_ops.autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+        # (16-bit autocast only: in fp32 training the 2-D layers stay MIOpen's)
+        wdt = train_ops.train_wdtype(x)
+        wdt = wdt if wdt in train_ops._TORCH_16 else None
         if STFT_D_HIP and wdt is not None and _freq_conv_ok(first):
             # the 1-channel first layer (its data-gradient was CK's slowest
             # conv kernel in the step) on the HIP training conv
             h = conv2d_freq(first, h, wdt)
             layers = layers[1:]
-        if (STFT_D_HIP and STFT_D_ROWS and wdt is not None and train_ops._io16(wdt) and layers
-                and h.dim() == 4 and _rows_ok(layers)):
-            # every remaining layer as one row-joined HIP conv on the
-            # row-padded layout (train_ops.Conv2dRowsHip16), the LeakyReLU
-            # between two layers fused into the next conv's input staging
-            T = h.shape[3]
-            lp = max(l.padding[1] for l in layers if isinstance(l, Conv2d))
-            L = train_ops.rows_len(T, lp)
-            R = train_ops.ROW_PAD
-            hp = torch.nn.functional.pad(h.to(train_ops._TORCH_16[wdt]), (lp, L - T - lp, R, R))
-            slope = 1.0
-            for layer in layers:
-                if isinstance(layer, LeakyReLU):
-                    slope = layer.negative_slope
-                    continue
-                w = layer.weight
-                hp = train_ops.Conv2dRowsHip16.apply(hp, w, layer.bias, layer.stride[0],
-                                                     layer.padding[1], lp, T, slope, wdt)
-                slope = 1.0
-            assert hp.shape[1] == 1 and hp.shape[2] == 1 + 2 * R
-            # [B, 1, T] like the reference's h.squeeze(1).squeeze(2) of [B, 1, 1, T]
-            return hp[:, :, R, lp:lp + T]
-        if STFT_D_HIP_ALL and wdt is not None and layers and all(
-                _freq_conv_ok(l) for l in layers if isinstance(l, Conv2d)):
-            # every remaining layer on the HIP training conv, the LeakyReLU
-            # between two layers fused into the next conv's input staging
-            # (and its derivative into that conv's data-gradient epilogue)
-            slope = 1.0
-            for layer in layers:
-                if isinstance(layer, LeakyReLU):
-                    slope = layer.negative_slope
-                else:
-                    h = conv2d_freq(layer, h, wdt, in_slope=slope)
-                    slope = 1.0
-            return h.squeeze(1).squeeze(2)
         if STFT_D_NHWC and h.device.type == "cuda":
             h = h.contiguous(memory_format=torch.channels_last)
             for layer in layers:
@@ -166,32 +132,10 @@ class STFTDiscriminator(nn.Module):
 
 
 STFT_D_HIP = True  # test switch: False keeps every STFT-discriminator conv on torch
-# layers 2+ as row-joined HIP convs on the row-padded layout (train_ops.Conv2dRowsHip16):
-# off by default - measured 82.3 vs 80.1 ms per B=32 step against MIOpen's
-# NHWC fp16 kernels (the 64-row tiles and the padded rows: see DESIGN 4f)
-STFT_D_ROWS = os.environ.get("VITS_STFT_D_ROWS", "0") != "0"
-
-
-def _rows_ok(layers) -> bool:
-    """Conv2d layers of Conv2dRowsHip16's form: groups 1, dilation 1, time
-    stride 1, no frequency padding, 'same' time padding (k1 = 2 p1 + 1),
-    k1 on the conv kernel's tap list, 64-multiple channel counts (K-chunks
-    within one frequency tap) - except the last layer's single output."""
-    convs = [l for l in layers if isinstance(l, Conv2d)]
-    lp = max(l.padding[1] for l in convs)
-    for l in convs:
-        if (l.groups != 1 or l.dilation != (1, 1) or l.stride[1] != 1 or l.padding[0] != 0
-                or 2 * l.padding[1] + 1 != l.kernel_size[1] or l.padding_mode != "zeros"
-                or l._forward_pre_hooks or l.in_channels % 16 != 0
-                or not train_ops._lib_k_ok(l.kernel_size[1], 1)):
-            return False
-    return lp >= 1
-# all STFT-discriminator layers (not only the first) on the HIP conv
-STFT_D_HIP_ALL = os.environ.get("VITS_STFT_D_HIP_ALL", "0") != "0"
 # channels-last operands for the STFT discriminators' MIOpen convs: its NHWC
 # solvers then run without the NCHW<->NHWC batched transposes around every
-# conv (train step 104.1 -> 101.3 ms); VITS_STFT_D_NHWC=0 restores NCHW
-STFT_D_NHWC = os.environ.get("VITS_STFT_D_NHWC", "1") != "0"
+# conv (train step 104.1 -> 101.3 ms)
+STFT_D_NHWC = True
 
 
 def _freq_conv_ok(layer) -> bool:
@@ -282,8 +226,7 @@ class GroupedSpectralNorm:
         # first, which conv2d_freq lowers onto the HIP conv): their W / sigma
         # is produced as the fp16 channels-last operand under autocast
         firsts = {id(sub.convs[0]) for sub in root.modules() if isinstance(sub, STFTDiscriminator)}
-        cl = (STFT_D_NHWC and not STFT_D_HIP_ALL and not STFT_D_ROWS
-              and os.environ.get("VITS_SN_CL", "1") != "0")  # A/B switch
+        cl = STFT_D_NHWC
         self.cl16 = [cl and isinstance(m, Conv2d) and id(m) not in firsts for m, _, _ in self.flat]
 
     def _fused_ok(self) -> bool:
@@ -363,14 +306,14 @@ class MultiWaveSTFTDiscriminator(nn.Module):
 # ---------------------------------------------------------------------------
 
 MPD_LRELU_SLOPE = 0.1  # modules.LRELU_SLOPE (models.py:347,374)
-_MPD_HIP = os.environ.get("VITS_MPD_HIP", "1") != "0"  # diagnostics switch
-MPD_GEMM = os.environ.get("VITS_MPD_GEMM", "1") != "0"  # im2col+GEMM for strided/grouped
+_MPD_HIP = True  # test switch: False keeps the MPD on torch
+MPD_GEMM = True  # im2col + GEMM for the strided / grouped layers
 
 
 def _hip_wdtype(x):
     if not _MPD_HIP or x.device.type != "cuda":
         return None
-    return train_ops.autocast_wdtype(x.device.type)
+    return train_ops.train_wdtype(x)
 
 
 def conv1d_gemm(x: torch.Tensor, w: torch.Tensor, bias, stride: int, padding: int,

@@ -127,15 +127,15 @@ def _conv_eff(conv: torch.nn.Module):
 # ---------------------------------------------------------------------------
 # grouped launches of the ResBlock2 branches (VITS_GROUP_BRANCHES=0: one
 # launch per conv, for A/B timing)
-_GROUP_BRANCHES = os.environ.get("VITS_GROUP_BRANCHES", "1") != "0"
+_GROUP_BRANCHES = True
 # fused ResBlock2 pairs on the 32/64-channel stages (VITS_FUSED_PAIRS=0: the
 # two-conv path, for A/B timing and the parity test of both)
-_FUSED_PAIRS = os.environ.get("VITS_FUSED_PAIRS", "1") != "0"
+_FUSED_PAIRS = True
 # 16-bit models: the last pairs of a stage's branches as one branch-mean
 # launch (vits_resblock_pair16_mean_forward); 0 = one accumulating launch each.
 # Used on the 32-channel stage (C5: 0.47 -> 0.41 ms); on the 64-channel one
 # the summing kernel reaches 256 VGPRs and lost (0.61 -> 0.69 ms)
-MEAN_PAIRS16 = os.environ.get("VITS_MEAN_PAIRS16", "1") != "0"
+MEAN_PAIRS16 = True
 # 16-bit models keep the decoder's activations 16-bit in HBM (as the
 # reference's .half() model holds them): every conv of the Generator reads and
 # writes its own 16-bit type (io16), halving the stage traffic.  C5 (B=4,
@@ -144,7 +144,7 @@ MEAN_PAIRS16 = os.environ.get("VITS_MEAN_PAIRS16", "1") != "0"
 # issue-bound rather than HBM-bound, so most of the gain is the global-memory
 # weight path these groups can take (conv1d.hip ga16, io16 = 2).
 # VITS_ACT16=0: fp32 activations (the 16-bit MFMA on fp32 I/O), for A/B.
-ACT16 = os.environ.get("VITS_ACT16", "1") != "0"
+ACT16 = True
 
 
 class GeneratorPlan:

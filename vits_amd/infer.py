@@ -201,6 +201,12 @@ class EmoVITS(object):
             pool, state = ops.numpy_draw_pool()
             wav, y_len = run(text_t, emo, sid, noise_start=pool, x_length=t_x)
             n, used = (int(v) for v in y_len[:, 0].tolist())  # (synchronises)
+            if n <= tyb and used == -2:
+                # every word of the pool was rejected (p < 2^-32): numpy's
+                # randint would go on drawing - advance past the pool and
+                # replay with the next words of the same stream
+                ops.numpy_draw_commit(state, ops.ED_DRAWS)
+                continue
             if n <= tyb:
                 if used < 0:
                     np.random.set_state(state)

@@ -34,10 +34,6 @@ class LayerNorm(nn.Module):
         self.beta = nn.Parameter(torch.zeros(channels))
 
     def forward(self, x):
-        if x.is_cuda and train_ops.LN_HIP:
-            # HIP forward / backward over the channel axis in place (no
-            # transposed copies); fp32 as autocast runs layer_norm
-            return train_ops.LayerNormHip.apply(x, self.gamma, self.beta, self.eps)
         y = F.layer_norm(x.transpose(1, -1), (self.channels,), self.gamma, self.beta, self.eps)
         return y.transpose(1, -1)
 

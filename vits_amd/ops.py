@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes as C
-import os
 import threading
 from dataclasses import dataclass, field
 from typing import Optional
@@ -116,10 +115,6 @@ X_TILE_FLOATS = {128: 2048, 256: 4096}                  # conv1d.hip XTile<BN>::
 # 64x128 89 -> 5; 64x256 is budgeted at 3: its k=7 convs run faster with the
 # bigger chunk); the K-chunk is sized so that LDS does not cut this further
 TILE_OCCUPANCY = {TILE_128x128: 3, TILE_64x256: 3, TILE_32x256: 4, TILE_64x128: 5}
-# experiment knob (tools/ab_*.sh): VITS_TILE_OCC="tile:wgs,..." overrides entries
-for _kv in filter(None, os.environ.get("VITS_TILE_OCC", "").split(",")):
-    _t, _o = _kv.split(":")
-    TILE_OCCUPANCY[int(_t)] = int(_o)
 LDS_BYTES_PER_CU = 160 * 1024
 
 
@@ -241,7 +236,7 @@ def _pick_tile_f32p(m: int, k: int) -> int:
 # chunk barriers) when the window of a 32-channel chunk fits the staging
 # budget (conv1d_impl.h XTile<BN, true, true>: 6144 / 10240 elements for 128
 # / 256 columns), else 16; VITS_F32P_KC=16 forces single slabs
-F32P_MAX_KC = int(os.environ.get("VITS_F32P_KC", "32"))
+F32P_MAX_KC = 32
 
 
 def _kc_f32p(cin_pad: int, k: int, dil: int, tile: int) -> int:
@@ -261,7 +256,7 @@ def _kc_f32p(cin_pad: int, k: int, dil: int, tile: int) -> int:
 
 # pre-split weights for split fp32 (VITS_SPLIT_W=0: the F32S kernel, which
 # splits the fp32 weight slabs per fragment in registers)
-SPLIT_W = os.environ.get("VITS_SPLIT_W", "1") != "0"
+SPLIT_W = True
 
 
 def split_planes(w: torch.Tensor) -> torch.Tensor:
@@ -288,7 +283,7 @@ def split_planes(w: torch.Tensor) -> torch.Tensor:
 # (F32P, tools/conv_bench.py on MI355X, r03) the 64-channel stage gains too
 # (k=11 c1 180 vs 122 TF/s exact, c2 138 vs 107, k=7 c1 154 vs 104; k=3 c2
 # 56 vs 60), the 32-channel one still does not (k=11 92 vs 108): 64 rows.
-F32S_MIN_ROWS = int(os.environ.get("VITS_F32S_MIN_ROWS", "0"))
+F32S_MIN_ROWS = 0
 
 
 def _f32s_min_rows() -> int:
@@ -343,7 +338,7 @@ def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
 # (engine.ACT16): the X window of a chunk stages at 2 bytes per element, so a
 # chunk can hold 32-64 channels instead of 16 (fewer barriers per tile).
 # VITS_LOWP_KCK caps kc * k (16: keep kc = 16, for A/B).
-LOWP_KCK = int(os.environ.get("VITS_LOWP_KCK", "512"))
+LOWP_KCK = 512
 
 
 def io16_kc(layer: PackedConv) -> int:
@@ -673,7 +668,7 @@ def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch
 
 # fused pairs of 16-bit models (csrc/resblock16.hip): VITS_FUSED_PAIRS16=0
 # keeps their two-conv path
-FUSED_PAIRS16 = os.environ.get("VITS_FUSED_PAIRS16", "1") != "0"
+FUSED_PAIRS16 = True
 
 
 def resblock_pair16_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -> bool:
@@ -876,11 +871,13 @@ def expand_durations(logw: torch.Tensor, m_p: torch.Tensor, s_p: torch.Tensor,
     m_p + noise * s_p * noise_scale over the static bucket t_y (0 past
     y_len), lens[i] = y_len * stage_mult[i].  ``noise`` is [B, C, t_y], or
     with ``noise_start`` (int32 [B]) a flat buffer read as EmoVITS slices it
-    (element (c, t) at s + c * y_len + t): ``noise_start`` is then int32
-    [B, ED_DRAWS] raw MT19937 words (``numpy_draw_pool``) from which the
+    (element (c, t) at s + c * y_len + t): ``noise_start`` is then an int32
+    [B, ED_DRAWS] pool of raw MT19937 words (``numpy_draw_pool``) from which the
     device draws s = np.random.randint(numel - C * y_len) exactly as numpy's
     legacy RandomState would, and ``lens`` gets one more row: the words
-    consumed per utterance (-1: the slice does not fit, z is zero)."""
+    consumed per utterance (-1: the slice does not fit; -2: every word of the
+    pool was rejected, the caller advances by the pool and calls again; z is
+    zero for both)."""
     require_device(logw, m_p, s_p, noise)
     B, C_, t_x = m_p.shape
     logw = logw.reshape(B, t_x).float().contiguous()
@@ -949,26 +946,6 @@ def layer_norm_channels(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Op
                                        scale, _ptr(pos), _ptr(pos_alpha),
                                        _stream_ptr(x.device)), "vits_layer_norm_channels")
     return out
-
-
-def layer_norm_channels_backward(x: torch.Tensor, gamma: Optional[torch.Tensor], dy: torch.Tensor,
-                                 eps: float = 1e-5, need_affine: bool = True):
-    """(dx, dgamma, dbeta) of y = LN_C(x) * gamma + beta on [B, C, T] fp32
-    contiguous x / dy (vits_layer_norm_channels_backward); dgamma / dbeta
-    None when not need_affine."""
-    require_device(x, gamma, dy)
-    assert x.is_contiguous() and dy.is_contiguous() and x.shape == dy.shape
-    B, Cc, T = x.shape
-    dx = torch.empty_like(x)
-    rows = B * ((T + 63) // 64)
-    dgp = torch.empty(rows, Cc, device=x.device) if need_affine else None
-    dbp = torch.empty(rows, Cc, device=x.device) if need_affine else None
-    check(_lib.load().vits_layer_norm_channels_backward(
-        x.data_ptr(), _ptr(gamma), dy.data_ptr(), dx.data_ptr(), _ptr(dgp), _ptr(dbp), B, Cc, T,
-        eps, _stream_ptr(x.device)), "vits_layer_norm_channels_backward")
-    if not need_affine:
-        return dx, None, None
-    return dx, dgp.sum(0), dbp.sum(0)
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, n_heads: int,

@@ -25,10 +25,15 @@ autocast convs round inputs/weights to fp16 and return fp16; here operands
 are rounded the same way but results stay fp32 (GradScaler overflow
 semantics are the same: an fp16-overflowing gradient becomes inf).
 
-``conv1d`` selects the path: inside a 16-bit autocast region on a ROCm
-device (the reference's ``fp16_run``) it is always the HIP path and raises if
-the library is missing; in fp32 training (autocast off) and on CPU it is the
-torch conv, i.e. the reference's own fp32 arithmetic.
+``conv1d`` selects the path (``train_wdtype``): on a ROCm device it is
+always a HIP path and raises if the library is missing - inside a 16-bit
+autocast region (the reference's ``fp16_run``) the 16-bit kernels with fp16
+activations, in fp32 training (autocast off, ``fp16_run: false``) the fp32
+kernels (``Conv1dHip32``: forward / input gradient on the split- or exact-
+fp32 MFMA conv of the inference path, weight gradient on the exact-fp32
+MFMA ``wgrad_f32_kernel``; fp32 activations, the reference's fp32
+precision).  On CPU, and with ``HIP_TRAIN = False`` (a test switch: the
+reference's own torch arithmetic on the same device), it is the torch conv.
 """
 from __future__ import annotations
 
@@ -43,9 +48,10 @@ from torch import nn
 from . import _lib
 from ._lib import (EPI_GATE, EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, TILE_128x128,
                    WDT_BF16, WDT_F16, WDT_F32, ConvWgradDesc, check)
+from . import engine
 from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
-                  layer_norm_channels, layer_norm_channels_backward, make_desc, make_out,
-                  weight_norm_effective)
+                  make_desc, make_out,
+                  pack_conv, to_lowp, weight_norm_effective)
 
 _TORCH_16 = {WDT_F16: torch.float16, WDT_BF16: torch.bfloat16}
 TRAIN_WDTYPE = WDT_F16  # the reference's autocast dtype (train_stft.py:165)
@@ -69,8 +75,7 @@ def _pick_tile_train(m: int, k: int, n_out: int | None) -> int:
 # kc * k <= TRAIN_KCK.  A chunk is one barrier-separated step of the
 # kernel's two-stage global->LDS pipeline; at kc = 16 a 1x1 conv has one
 # MFMA k-step per chunk and waits on every chunk's loads.
-TRAIN_KCK = int(os.environ.get("VITS_TRAIN_KCK", "64"))
-_GA_ALL = os.environ.get("VITS_GA16") == "2"  # weights from global memory: no W LDS budget
+TRAIN_KCK = 64
 _TILE_BM = {TILE_128x128: 128, TILE_64x128: 64, TILE_64x256: 64, TILE_32x256: 32}
 _TILE_BN = {TILE_128x128: 128, TILE_64x128: 128, TILE_64x256: 256, TILE_32x256: 256}
 
@@ -85,14 +90,14 @@ def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
     xbudget = (6144 if bn <= 128 else 10240) if io16 else (3072 if bn <= 128 else 5120)
     for kc in (64, 48, 32):
         if (kc * k <= TRAIN_KCK and cin_pad % kc == 0
-                and (_GA_ALL or kc * k * bm // 2 <= 6144)
+                and kc * k * bm // 2 <= 6144
                 and kc * xrs <= xbudget):
             return kc
     return 16
 
 
 # per-call weight packs by call site (tools/pack_census.py; VITS_PACK_TRACE=1)
-PACK_TRACE = collections.Counter() if os.environ.get("VITS_PACK_TRACE") == "1" else None
+PACK_TRACE = None  # tools/pack_census.py sets a collections.Counter()
 
 
 def _trace_pack(kind, shape):
@@ -170,7 +175,7 @@ def _layers16(pre, shape, dil: int, pad_left: int, wdtype: int, bias, n_out: int
 _PREPACK: dict = {}
 
 
-PREPACK = os.environ.get("VITS_PREPACK", "1") != "0"  # A/B switch
+PREPACK = True
 
 
 @contextlib.contextmanager
@@ -182,7 +187,7 @@ def prepacked(net: nn.Module):
     ``vits_conv1d_pack16_pairs`` launch per 48 layers instead of one
     ``vits_conv1d_pack16_pair`` launch per conv call.  The images are valid
     for this scope only (the weights change at the next optimizer step)."""
-    wdt = autocast_wdtype("cuda")
+    wdt = autocast_wdtype("cuda") if HIP_TRAIN else None
     mods = []
     if PREPACK and wdt is not None and _io16(wdt):
         mods = [m for m in net.modules() if supported(m)
@@ -411,6 +416,140 @@ class GateHip(torch.autograd.Function):
         return dx, dg
 
 
+def _pack32(w32: torch.Tensor, dil: int, pad_left: int, bias=None, gate: bool = False,
+            transpose: bool = False) -> PackedConv:
+    """fp32 image of a [cout, cin, k] weight for the fp32 training convs: the
+    inference packing (ops.pack_conv) in the engine's fp32 arithmetic
+    (engine.FP32_WDTYPE: split fp32 - three exact bf16 planes - on >= 64-row
+    layers, exact fp32 otherwise).  transpose: the input-gradient image (rows
+    cin, channels cout, taps reversed, pad' = (k-1)*dil - pad)."""
+    _trace_pack("pack32", w32.shape)
+    k = w32.shape[2]
+    if transpose:
+        w32 = w32.transpose(0, 1).flip(2)
+        pad_left = (k - 1) * dil - pad_left
+    layer = pack_conv(w32, bias, dilation=dil, padding=pad_left, gate=gate)
+    return to_lowp(layer, engine.FP32_WDTYPE)
+
+
+class Conv1dHip32(torch.autograd.Function):
+    """y = conv1d(leaky_relu(x, in_slope), weight, bias, dilation, padding)
+    (+ res) in fp32 training (autocast off): fp32 activations and weights,
+    fp32 arithmetic throughout.  Forward and input gradient run the
+    inference path's fp32 conv (split fp32 / exact fp32 MFMA, leaky-relu
+    prologue and its derivative fused as in Conv1dHip16), the weight / bias
+    gradient the exact-fp32 MFMA split-K kernel (vits_conv1d_wgrad_split,
+    VITS_WDT_F32)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, dilation: int, padding: int, in_slope: float, res=None):
+        if x.stride(2) != 1:
+            x = x.contiguous()
+        w32 = weight.detach().float().contiguous()
+        k = w32.shape[2]
+        n_out = x.shape[2] + 2 * padding - (k - 1) * dilation
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        layer = _pack32(w32, dilation, padding, b32)
+        ctx.layer_t = (_pack32(w32, dilation, padding, transpose=True)
+                       if ctx.needs_input_grad[0] else None)
+        if res is not None:
+            assert res.dtype == torch.float32 and res.shape == (x.shape[0], w32.shape[0], n_out)
+            if res.stride(2) != 1:
+                res = res.contiguous()
+        y = _run(x, layer, n_out, in_slope, res=res)
+        ctx.save_for_backward(x, w32)
+        ctx.conf = (dilation, padding, in_slope, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w32 = ctx.saved_tensors
+        dil, pad, slope, has_bias = ctx.conf
+        k = w32.shape[2]
+        dy = dy.float()
+        if dy.stride(2) != 1:
+            dy = dy.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _run(dy, ctx.layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
+                      gmask_slope=slope)
+        ctx.layer_t = None
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dw, db = wgrad(dy, x, k, dil, pad, slope, with_bias=has_bias, wdtype=WDT_F32,
+                           split=True)
+        dres = dy if (len(ctx.needs_input_grad) > 6 and ctx.needs_input_grad[6]) else None
+        return dx, dw, db, None, None, None, dres
+
+
+class ConvGateHip32(torch.autograd.Function):
+    """ConvGateHip16 in fp32 training: acts = tanh(xin_a + g_a) *
+    sigmoid(xin_b + g_b), xin = conv1d(leaky_relu(x, in_slope), W) + b, one
+    conv launch (GATE epilogue on gate-interleaved rows, the pre-activation
+    xin written for the backward); backward: the fp32 gate backward kernel
+    (dxin, the cond gradient summed over time), then Conv1dHip32's input /
+    weight gradient kernels.  All fp32."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, g, dilation: int, padding: int, in_slope: float):
+        if x.stride(2) != 1:
+            x = x.contiguous()
+        B, _, T = x.shape
+        w32 = weight.detach().float().contiguous()
+        cout, cin, k = w32.shape
+        H = cout // 2
+        n_out = T + 2 * padding - (k - 1) * dilation
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        layer = _pack32(w32, dilation, padding, b32, gate=True)
+        ctx.layer_t = (_pack32(w32, dilation, padding, transpose=True)
+                       if ctx.needs_input_grad[0] else None)
+        acts = torch.empty(B, H, n_out, device=x.device, dtype=torch.float32)
+        xin = torch.empty(B, cout, n_out, device=x.device, dtype=torch.float32)
+        cond = None
+        if g is not None:
+            cond = g.detach()
+            if cond.dim() == 3:
+                cond = cond[:, :, 0]
+            if cond.stride(1) != 1:
+                cond = cond.contiguous()
+        d = make_desc(layer, x, make_out(acts), out1=make_out(xin), in_slope=in_slope, tin=T,
+                      n_out=n_out, cond=cond)
+        conv1d_launch(d, B, x.device)
+        ctx.g_shape = None if g is None else tuple(g.shape)
+        ctx.save_for_backward(x, w32, xin, cond)
+        ctx.conf = (dilation, padding, in_slope, bias is not None)
+        return acts
+
+    @staticmethod
+    def backward(ctx, dacts):
+        x, w32, xin, g = ctx.saved_tensors
+        dil, pad, slope, has_bias = ctx.conf
+        B, C2, T = xin.shape
+        H = C2 // 2
+        k = w32.shape[2]
+        dacts = dacts.float()
+        if dacts.stride(2) != 1:
+            dacts = dacts.contiguous()
+        dxin = torch.empty(B, C2, T, device=xin.device, dtype=torch.float32)
+        want_dg = g is not None and ctx.needs_input_grad[3]
+        dg = torch.empty(B, C2, device=xin.device, dtype=torch.float32) if want_dg else None
+        check(_lib.load().vits_gate_backward(
+            dacts.data_ptr(), dacts.stride(0), dacts.stride(1), xin.data_ptr(), xin.stride(0),
+            xin.stride(1), None if g is None else g.data_ptr(), 0 if g is None else g.stride(0),
+            dxin.data_ptr(), dxin.stride(0), dxin.stride(1), None if dg is None else dg.data_ptr(),
+            B, H, T, _stream_ptr(xin.device)), "vits_gate_backward")
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _run(dxin, ctx.layer_t, x.shape[2], gmask=x if slope != 1.0 else None,
+                      gmask_slope=slope)
+        ctx.layer_t = None
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dw, db = wgrad(dxin, x, k, dil, pad, slope, with_bias=has_bias, wdtype=WDT_F32,
+                           split=True)
+        if dg is not None and len(ctx.g_shape) == 3:
+            dg = dg.unsqueeze(-1)
+        return dx, dw, db, dg, None, None, None
+
+
 class Conv1dHip16(torch.autograd.Function):
     """Conv1dHip with 16-bit activations: x, y, dY and dX are tensors of the
     operand type (fp16 under the reference's fp16 autocast, whose convs
@@ -476,42 +615,6 @@ class Conv1dHip16(torch.autograd.Function):
             grads.append(dy if ctx.needs_input_grad[7] else None)
         grads += [None] * (len(ctx.needs_input_grad) - len(grads))
         return tuple(grads)
-
-
-# modules.LayerNorm on the HIP kernels on the GPU (VITS_LN_HIP=1).  Off by
-# default: measured 78.4 vs 77.4 ms per B=32 train step against torch's
-# layer_norm (the per-channel wave reductions of dgamma / dbeta and the
-# (utterance, 64-frame) grid - 256 workgroups at T=500 - lose to it)
-LN_HIP = os.environ.get("VITS_LN_HIP", "0") != "0"
-
-
-class LayerNormHip(torch.autograd.Function):
-    """modules.LayerNorm (modules.py:33-44) on the GPU: y = LN over C of
-    [B, C, T] * gamma + beta in fp32 (the reference's F.layer_norm, which
-    autocast runs in fp32, on a transposed view), forward
-    vits_layer_norm_channels, backward vits_layer_norm_channels_backward
-    (dx, and dgamma / dbeta from per-tile partial sums)."""
-
-    @staticmethod
-    def forward(ctx, x, gamma, beta, eps: float):
-        x32 = x.detach().float().contiguous()
-        g = gamma.detach().float().contiguous()
-        b = beta.detach().float().contiguous()
-        y = layer_norm_channels(x32, g, b, eps)
-        ctx.save_for_backward(x32, g)
-        ctx.eps = eps
-        ctx.xdtype = x.dtype
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x32, g = ctx.saved_tensors
-        need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        dx, dg, db = layer_norm_channels_backward(x32, g, dy.float().contiguous(), ctx.eps,
-                                                  need_affine)
-        return (dx.to(ctx.xdtype) if ctx.needs_input_grad[0] else None,
-                dg if ctx.needs_input_grad[1] else None,
-                db if ctx.needs_input_grad[2] else None, None)
 
 
 class GateHip16(torch.autograd.Function):
@@ -595,7 +698,7 @@ def wn_update(x: torch.Tensor, rs: torch.Tensor, mask: torch.Tensor, out):
     """(x', x16', out') of WN's residual / skip update (WNUpdate16) when it
     applies: an fp16-autocast training step on the GPU, fp32 contiguous x /
     out / mask and a 16-bit rs; None otherwise (the caller runs torch)."""
-    wdt = autocast_wdtype() if x.device.type == "cuda" else None
+    wdt = train_wdtype(x)
     if (wdt is None or not _io16(wdt) or rs.dtype != _TORCH_16[wdt] or x.dtype != torch.float32
             or mask.dtype != torch.float32 or (out is not None and out.dtype != torch.float32)):
         return None
@@ -607,7 +710,7 @@ def wn_update(x: torch.Tensor, rs: torch.Tensor, mask: torch.Tensor, out):
 
 # 16-bit activations for the training convs / gates under fp16 autocast (the
 # reference's autocast convs return fp16); False: the fp32-I/O kernels
-TRAIN_IO16 = os.environ.get("VITS_TRAIN_IO16", "1") != "0"
+TRAIN_IO16 = True
 
 
 def _io16(wdt) -> bool:
@@ -619,8 +722,10 @@ def conv1d_hip(x: torch.Tensor, w: torch.Tensor, bias, dilation: int, padding: i
                pre=None) -> torch.Tensor:
     """The HIP training conv of operand type ``wdt`` (+ ``residual``): 16-bit
     activations (Conv1dHip16; x cast to fp16 first, as autocast casts a
-    conv's input; the residual added in the epilogue) or fp32 activations
-    (Conv1dHip).  ``pre``: the weight's prepacked images (``prepacked``)."""
+    conv's input; the residual added in the epilogue), fp32 training
+    (WDT_F32: Conv1dHip32, fp32 arithmetic, the residual in the epilogue)
+    or fp32 activations with 16-bit operands (Conv1dHip).  ``pre``: the
+    weight's prepacked images (``prepacked``)."""
     if _io16(wdt):
         t16 = _TORCH_16[wdt]
         x16 = x if x.dtype == t16 else x.to(t16)
@@ -629,18 +734,22 @@ def conv1d_hip(x: torch.Tensor, w: torch.Tensor, bias, dilation: int, padding: i
             return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt,
                                      None, pre) + residual
         return Conv1dHip16.apply(x16, w, bias, dilation, padding, in_slope, wdt, residual, pre)
+    if wdt == WDT_F32:
+        res = None if residual is None else residual.float()
+        return Conv1dHip32.apply(x.float(), w, bias, dilation, padding, in_slope, res)
     y = Conv1dHip.apply(x, w, bias, dilation, padding, in_slope, wdt)
     return y if residual is None else y + residual
 
 
 def gate(x: torch.Tensor, g) -> torch.Tensor:
-    """The WN / ResBlock2 gate: the HIP op inside a 16-bit autocast region on
-    a ROCm device (where the convs around it are HIP too), torch otherwise."""
-    wdt = autocast_wdtype() if x.device.type == "cuda" else None
+    """The WN / ResBlock2 gate: the HIP op on a ROCm device (16-bit under
+    fp16 autocast, fp32 in fp32 training; the convs around it are HIP too),
+    torch on CPU / with HIP_TRAIN off."""
+    wdt = train_wdtype(x)
     if wdt is not None and _io16(wdt) and x.dtype == _TORCH_16[wdt]:
         g16 = None if g is None else g.to(x.dtype)
         return GateHip16.apply(x, g16, wdt)
-    if x.device.type == "cuda" and wdt is not None:
+    if wdt is not None:
         return GateHip.apply(x, g)
     H = x.shape[1] // 2
     if g is not None:
@@ -665,6 +774,24 @@ def autocast_wdtype(device_type: str = "cuda"):
         return None
     dt = torch.get_autocast_dtype(device_type)
     return {torch.float16: WDT_F16, torch.bfloat16: WDT_BF16}.get(dt)
+
+
+# test switch: False runs every training conv / gate on torch (the
+# reference's own arithmetic, MIOpen) on the same device
+HIP_TRAIN = True
+
+
+def train_wdtype(x: torch.Tensor):
+    """Operand type of the HIP training kernels for an op on ``x``: the
+    autocast dtype inside a 16-bit autocast region, WDT_F32 in fp32
+    training (autocast off: the reference's fp16_run = false), None on CPU,
+    under another autocast dtype, or with HIP_TRAIN off (torch path)."""
+    if not HIP_TRAIN or x.device.type != "cuda":
+        return None
+    wdt = autocast_wdtype("cuda")
+    if wdt is not None:
+        return wdt
+    return None if torch.is_autocast_enabled("cuda") else WDT_F32
 
 
 def module_weight(module: nn.Module) -> torch.Tensor:
@@ -696,24 +823,14 @@ def conv1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0,
     Inside a 16-bit autocast region on a ROCm device (the reference's
     ``fp16_run`` training, train_stft.py:165,216) this is the HIP training
     conv with operands of the autocast dtype.  Outside autocast the reference
-    computes the conv in fp32, and so does this (torch conv): the fp32
-    training mode keeps the reference's precision.  On CPU it is the torch
-    conv."""
-    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+    computes the conv in fp32, and so does this: the fp32 HIP training conv
+    (Conv1dHip32).  On CPU it is the torch conv."""
+    wdt = train_wdtype(x)
     if wdt is None or not supported(module):
         if in_slope != 1.0:
             x = F.leaky_relu(x, in_slope)
         return module(x) if residual is None else module(x) + residual
     w = weight_norm_effective(module)
-    if (GEMM_1X1_MAX_T and w.shape[2] == 1 and module.padding[0] == 0 and in_slope == 1.0
-            and residual is None and x.shape[2] <= GEMM_1X1_MAX_T and _io16(wdt)):
-        # a 1x1 conv on a short time axis (the text encoder's q/k/v/o and
-        # FFN projections, T = 100) is a plain batched GEMM: hipBLASLt via
-        # torch.matmul under autocast (the tiled conv kernel leaves most of a
-        # 128-column tile and most CUs idle at B*ceil(T/128) workgroups)
-        t16 = _TORCH_16[wdt]
-        y = torch.matmul(w[:, :, 0].to(t16), x.to(t16))
-        return y if module.bias is None else y + module.bias.to(t16)[:, None]
     ent = _PREPACK.get(module)
     pre = ent[1] if (ent is not None and ent[0] is w and ent[2] == wdt and not ent[3]) else None
     return conv1d_hip(x, w, module.bias, module.dilation[0], module.padding[0], in_slope, wdt,
@@ -728,9 +845,9 @@ def conv1d_cat(modules, x: torch.Tensor):
     GEMM - no adds) and one weight gradient instead of three each.  Returns
     the outputs as channel slices of one [B, sum(C_out), T] tensor, or None
     where conv1d would not run the modules on the HIP kernels."""
-    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+    wdt = train_wdtype(x)
     m0 = modules[0]
-    if (wdt is None or not _io16(wdt) or not all(supported(m) for m in modules)
+    if (wdt is None or not (_io16(wdt) or wdt == WDT_F32) or not all(supported(m) for m in modules)
             or any(m.kernel_size != m0.kernel_size or m.dilation != m0.dilation
                    or m.padding != m0.padding or m.in_channels != m0.in_channels
                    or (m.bias is None) != (m0.bias is None) for m in modules)):
@@ -739,10 +856,6 @@ def conv1d_cat(modules, x: torch.Tensor):
     b = None if m0.bias is None else torch.cat([m.bias for m in modules], 0)
     y = conv1d_hip(x, w, b, m0.dilation[0], m0.padding[0], 1.0, wdt)
     return y.split([m.out_channels for m in modules], 1)
-
-
-# 1x1 training convs with T <= this run as hipBLASLt GEMMs (0: always the HIP conv)
-GEMM_1X1_MAX_T = int(os.environ.get("VITS_TRAIN_GEMM1X1", "0"))
 
 
 # ---------------------------------------------------------------------------
@@ -831,13 +944,13 @@ def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) 
     """``module(leaky_relu(x, in_slope))`` for an nn.ConvTranspose1d
     (optionally legacy-weight-normed, output_padding 0, groups 1, dilation 1).
 
-    Inside a 16-bit autocast region on a ROCm device: the polyphase lowering
+    On a ROCm device (fp16 autocast or fp32 training): the polyphase lowering
     on the HIP training conv - one stride-1 Conv1dHip (forward, input and
     weight gradient on MFMA) over phase-stacked weight rows, the leaky-relu
     fused as its prologue, then one interleave of the phases into time.
     The weight gradient flows back through the (differentiable) gather that
     builds the phase weights.  Elsewhere: the torch module (MIOpen / CPU)."""
-    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
+    wdt = train_wdtype(x)
     ok = (isinstance(module, nn.ConvTranspose1d) and module.groups == 1
           and module.dilation == (1,) and module.output_padding == (0,)
           and module.padding_mode == "zeros")
@@ -865,236 +978,13 @@ def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) 
 
 
 # ---------------------------------------------------------------------------
-# MultiHeadAttention.attention (attentions.py:85-100) in training
-# ---------------------------------------------------------------------------
-
-
-class AttentionHip(torch.autograd.Function):
-    """out = dropout(softmax(masked_fill(q k^T / sqrt(D), mask == 0, -1e4))) v
-    on [B, H*D, T] channel-major q / k / v (the projection convs' outputs,
-    no transposes), mask = the outer product of the length mask, fp32 MFMA
-    (vits_attention_train_forward / _backward: the forward keeps O and each
-    query's softmax max and normaliser, the backward recomputes P).  ``keep`` (uint8 [B,
-    H, T, T] or None) is nn.Dropout's keep mask, applied as keep / (1 - p)."""
-
-    @staticmethod
-    def forward(ctx, q, k, v, lengths, heads: int, keep, p: float):
-        B, C, T = q.shape
-        D = C // heads
-        dt = q.dtype
-        code = WDT_F16 if dt == torch.float16 else WDT_F32
-        q, k, v = q.contiguous(), k.to(dt).contiguous(), v.to(dt).contiguous()
-        out = torch.empty_like(q)
-        lse = torch.empty(B, heads, T, 2, device=q.device, dtype=torch.float32)  # (m, 1/l)
-        scale = 1.0 / (1.0 - p) if keep is not None else 1.0
-        check(_lib.load().vits_attention_train_forward(
-            q.data_ptr(), k.data_ptr(), v.data_ptr(), None if keep is None else keep.data_ptr(),
-            scale, out.data_ptr(), lse.data_ptr(), B, heads, D, T, lengths.data_ptr(), code,
-            _stream_ptr(q.device)), "vits_attention_train_forward")
-        ctx.save_for_backward(q, k, v, out, lse, lengths, keep)
-        ctx.conf = (heads, D, code, scale)
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        q, k, v, out, lse, lengths, keep = ctx.saved_tensors
-        heads, D, code, scale = ctx.conf
-        B, C, T = q.shape
-        dout = dout.to(q.dtype).contiguous()
-        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        delta = torch.empty(B, heads, T, device=q.device, dtype=torch.float32)
-        check(_lib.load().vits_attention_train_backward(
-            q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
-            None if keep is None else keep.data_ptr(), scale, lse.data_ptr(), delta.data_ptr(),
-            dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, heads, D, T, lengths.data_ptr(), code,
-            _stream_ptr(q.device)), "vits_attention_train_backward")
-        return dq, dk, dv, None, None, None, None
-
-
-# the HIP training attention (AttentionHip) in MultiHeadAttention: off by
-# default - measured 82.3 vs 80.5 ms per B=32 step against torch's
-# batched-GEMM attention (fp32 32x32x2 MFMAs, one wave per 32 queries: 256
-# single-wave workgroups at T=100 leave the chip latency-bound)
-ATTN_HIP = os.environ.get("VITS_ATTN_HIP", "0") != "0"
-
-
-def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
-              lengths: torch.Tensor | None, p_drop: float, training: bool):
-    """MultiHeadAttention.attention's output on the HIP training kernels, or
-    None when they do not apply (CPU, no lengths, autocast off, head dim not
-    in 32/64/96/128, q / k / v not of one length): the caller runs torch."""
-    wdt = autocast_wdtype("cuda") if q.device.type == "cuda" else None
-    D = q.shape[1] // heads
-    if (not ATTN_HIP or wdt is None or lengths is None or D not in (32, 64, 96, 128) or q.shape != k.shape
-            or k.shape != v.shape or q.dtype not in (torch.float16, torch.float32)):
-        return None
-    keep = None
-    if training and p_drop > 0:
-        B, _, T = q.shape
-        # nn.Dropout's draw: keep with probability 1 - p (device RNG, graph-safe)
-        keep = (torch.rand(B, heads, T, T, device=q.device) >= p_drop).to(torch.uint8)
-    return AttentionHip.apply(q, k, v, lengths.to(torch.int32).contiguous(), heads, keep,
-                              float(p_drop))
-
-
-# ---------------------------------------------------------------------------
-# STFT-discriminator Conv2d layers (mrd.py:122-133) on the HIP training conv
-# ---------------------------------------------------------------------------
-# Row-padded layout of the activations between the layers: [B, C, F + 4, L],
-# frequency rows f at row f + 2 (two zero rows at each end: the input
-# gradient's phase convs read two rows past either end), time t at column
-# p1 + t of an L = round_up(T + 2 p1, 4) row (zeros in the pad columns:
-# the next layer's zero padding along time).  Every layer is ONE row-joined
-# conv (vits_conv1d_desc.x_rowlen / x_cgroup / y_rowlen): columns n = f_out
-# * L + t, virtual input channels v = i * C + c (frequency tap i), k1 time
-# taps; output row f_out reads input rows s0 * f_out + i.
-ROW_PAD = 2
-
-
-def rows_len(T: int, p1: int) -> int:
-    return (T + 2 * p1 + 3) // 4 * 4
-
-
-def _pack16_img(w3: torch.Tensor, transpose: bool, wdtype: int) -> torch.Tensor:
-    """16-bit image of a [cout][cin][k] fp32 weight (vits_conv1d_pack16)."""
-    cout, cin, k = w3.shape
-    rows, chans = (cin, cout) if transpose else (cout, cin)
-    m_pad, cin_pad = (rows + 127) // 128 * 128, (chans + 15) // 16 * 16
-    img = torch.empty(cin_pad // 16, k, 2, m_pad, 8, dtype=_TORCH_16[wdtype], device=w3.device)
-    check(_lib.load().vits_conv1d_pack16(
-        w3.data_ptr(), cout, cin, k, int(transpose), img.data_ptr(), m_pad, cin_pad, wdtype,
-        None, 0, _stream_ptr(w3.device)), "vits_conv1d_pack16")
-    return img
-
-
-def _rows_desc(img, wdtype, rows, chans, k, pad_left, x, x_off, x_cstride, x_bstride, x_rowmul,
-               x_cgroup, x_gstride, L, n_rows_out, y, y_off, y_cstride, y_bstride, y_rowmul,
-               lp, T, in_slope, bias=None, gmask=None, gmask_off=0, gmask_slope=1.0):
-    tile = _pick_tile_train(rows, k, n_rows_out * L)
-    kc = _train_kc(img.shape[0] * 16, k, 1, tile, True)
-    while x_cgroup and x_cgroup % kc:
-        kc //= 2
-    d = _lib.ConvDesc()
-    d.x = x.data_ptr() + x.element_size() * x_off
-    d.io16 = 1
-    d.x_bstride, d.x_cstride, d.x_tstride = x_bstride, x_cstride, 1
-    d.cin = chans
-    d.tin = n_rows_out * L
-    d.in_slope = in_slope
-    d.w = img.data_ptr()
-    d.m, d.m_pad, d.cin_pad, d.kc = rows, img.shape[3], img.shape[0] * 16, kc
-    d.k, d.dil, d.pad_left = k, 1, pad_left
-    d.n_out = n_rows_out * L
-    d.tile, d.epi = tile, EPI_STORE
-    d.bias = None if bias is None else bias.data_ptr()
-    d.split = rows
-    d.lengths = None
-    d.out0 = make_out(y)
-    d.out0.y = y.data_ptr() + y.element_size() * y_off
-    d.out0.y_bstride, d.out0.y_cstride = y_bstride, y_cstride
-    d.out1 = make_out(y)
-    d.wdtype = wdtype
-    if gmask is not None:
-        d.gmask = gmask.data_ptr() + gmask.element_size() * gmask_off
-        d.gmask_bstride, d.gmask_cstride = gmask.stride(0), gmask.stride(1)
-        d.gmask_slope = gmask_slope
-    d.x_rowlen, d.x_rowmul, d.x_cgroup, d.x_gstride = L, x_rowmul, x_cgroup, x_gstride
-    d.y_rowlen, d.y_rowmul, d.y_rowpad, d.y_rowvalid = L, y_rowmul, lp, T
-    return d
-
-
-class Conv2dRowsHip16(torch.autograd.Function):
-    """Conv2d(C, O, (k0, k1), stride (s0, 1), padding (0, p1)) of
-    leaky_relu(x, in_slope) on the row-padded fp16 layout (see ROW_PAD; lp =
-    the layout's pad columns, >= p1; T valid columns per row):
-    x [B, C, F + 4, L] -> y [B, O, F_out + 4, L], F_out = (F - k0) // s0 + 1.
-    Forward: one row-joined conv over virtual channels (i, c).  Input
-    gradient: s0 phase convs (input rows s0 q + rho take the taps i = rho +
-    s0 i', reading output-gradient rows q - i'), the leaky-relu derivative of
-    x in their epilogue.  Weight / bias gradient: the row-joined split-K
-    wgrad over (b, f_out, t).  fp16 operands, fp32 accumulation, dW fp32."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias, s0: int, p1: int, lp: int, T: int, in_slope: float,
-                wdtype: int):
-        B, C, Fp, L = x.shape
-        F_ = Fp - 2 * ROW_PAD
-        O, _, k0, k1 = weight.shape
-        F_out = (F_ - k0) // s0 + 1
-        w32 = weight.detach().float()
-        wv = w32.permute(0, 2, 1, 3).reshape(O, k0 * C, k1).contiguous()  # v = i * C + c
-        img = _pack16_img(wv, False, wdtype)
-        y = torch.zeros(B, O, F_out + 2 * ROW_PAD, L, device=x.device, dtype=x.dtype)
-        b32 = None if bias is None else bias.detach().float().contiguous()
-        d = _rows_desc(img, wdtype, O, k0 * C, k1, p1, x, ROW_PAD * L, Fp * L, C * Fp * L,
-                       s0 * L, C if k0 > 1 else 0, L, L, F_out, y, ROW_PAD * L, y.stride(1),
-                       y.stride(0), L, lp, T, in_slope, bias=b32)
-        conv1d_launch(d, B, x.device)
-        ctx.save_for_backward(x, w32)
-        ctx.conf = (s0, p1, lp, T, in_slope, wdtype, bias is not None, F_out)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w32 = ctx.saved_tensors
-        s0, p1, lp, T, slope, wdtype, has_bias, F_out = ctx.conf
-        B, C, Fp, L = x.shape
-        F_ = Fp - 2 * ROW_PAD
-        O, _, k0, k1 = w32.shape
-        dy = dy.to(x.dtype).contiguous()
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.zeros_like(x)
-            for rho in range(s0):
-                taps = list(range(rho, k0, s0))            # i = rho + s0 * i'
-                Q = (F_ - rho + s0 - 1) // s0               # input rows s0 q + rho < F
-                if not taps or Q <= 0:
-                    continue
-                # [(i', o)][c][j] -> rows c, virtual channels (i', o), taps reversed
-                # (a slice, not an index list: no host->device copy under capture)
-                wp = w32[:, :, rho::s0, :].permute(2, 0, 1, 3).reshape(len(taps) * O, C, k1)
-                img = _pack16_img(wp.contiguous(), True, wdtype)
-                # (one tap: the virtual channels are the plain channels o)
-                cg = O if len(taps) > 1 else 0
-                d = _rows_desc(img, wdtype, C, len(taps) * O, k1, k1 - 1 - p1, dy, ROW_PAD * L,
-                               dy.stride(1), dy.stride(0), L, cg, -L, L, Q, dx,
-                               (ROW_PAD + rho) * L, dx.stride(1), dx.stride(0), s0 * L, lp, T, 1.0,
-                               gmask=x if slope != 1.0 else None,
-                               gmask_off=(ROW_PAD + rho) * L, gmask_slope=slope)
-                conv1d_launch(d, B, x.device)
-        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            dwv = torch.empty(O, k0 * C, k1, device=x.device, dtype=torch.float32)
-            db = torch.empty(O, device=x.device, dtype=torch.float32) if has_bias else None
-            wd = _lib.ConvWgradDesc()
-            wd.dy = dy.data_ptr() + dy.element_size() * ROW_PAD * L
-            wd.dy_bstride, wd.dy_cstride, wd.cout = dy.stride(0), dy.stride(1), O
-            wd.x = x.data_ptr() + x.element_size() * ROW_PAD * L
-            wd.x_bstride, wd.x_cstride, wd.cin = x.stride(0), x.stride(1), k0 * C
-            wd.tin, wd.n_out, wd.k, wd.dil, wd.pad_left = F_out * L, F_out * L, k1, 1, p1
-            wd.in_slope = slope
-            wd.dw_t = dwv.data_ptr()
-            wd.dbias = None if db is None else db.data_ptr()
-            wd.wdtype = wdtype
-            wd.io16 = 1
-            wd.x_rowlen, wd.x_rowmul, wd.x_cgroup, wd.x_gstride = L, s0 * L, C if k0 > 1 else 0, L
-            lib = _lib.load()
-            nws = int(lib.vits_conv1d_wgrad_workspace(wd, B))
-            ws = torch.empty(max(nws, 1), device=x.device, dtype=torch.float32)
-            check(lib.vits_conv1d_wgrad_split(wd, B, ws.data_ptr(), nws, _stream_ptr(x.device)),
-                  "vits_conv1d_wgrad_split")
-            dw = dwv.view(O, k0, C, k1).permute(0, 2, 1, 3).contiguous()
-        return dx, dw, db, None, None, None, None, None, None
-
-
-
-# ---------------------------------------------------------------------------
 # conv -> gate as one launch (WN modules.py:136-146, ResBlock2 modules.py:252-255)
 # ---------------------------------------------------------------------------
 # in_layer / convs1 convs whose output only feeds the tanh * sigmoid gate run
 # the GATE epilogue (gate-interleaved weight rows) and write the
 # pre-activation for the gate's backward in the same launch; VITS_GATE_FUSED=0
 # keeps the separate conv + GateHip16 kernels
-GATE_FUSED = os.environ.get("VITS_GATE_FUSED", "1") != "0"
+GATE_FUSED = True
 
 
 def _pack16_pair_gate(w32, wdtype):
@@ -1199,7 +1089,7 @@ class ConvGateHip16(torch.autograd.Function):
         return (dx, dw, db, dg, None, None, None, None, None, None)
 
 
-COND_F32 = os.environ.get("VITS_COND_F32", "1") != "0"  # A/B switch
+COND_F32 = True
 
 
 def cond_f32(g: torch.Tensor | None):
@@ -1214,13 +1104,17 @@ def cond_f32(g: torch.Tensor | None):
 
 def conv1d_gate(module: nn.Module, x: torch.Tensor, g, in_slope: float = 1.0, g16=None):
     """gate(module(leaky_relu(x, in_slope)), g) (WN / ResBlock2, the conv's
-    output feeding only the gate) as one ConvGateHip16 launch inside a 16-bit
-    autocast region on a ROCm device; None when that does not apply (the
-    caller runs conv1d + gate)."""
-    wdt = autocast_wdtype(x.device.type) if x.device.type == "cuda" else None
-    if (not GATE_FUSED or wdt is None or not _io16(wdt) or not supported(module)
-            or module.out_channels % 2):
+    output feeding only the gate) as one conv launch on a ROCm device
+    (ConvGateHip16 under fp16 autocast, ConvGateHip32 in fp32 training);
+    None when that does not apply (the caller runs conv1d + gate)."""
+    wdt = train_wdtype(x)
+    if (not GATE_FUSED or wdt is None or not (_io16(wdt) or wdt == WDT_F32)
+            or not supported(module) or module.out_channels % 2):
         return None
+    if wdt == WDT_F32:
+        cond = None if g is None else g.float()
+        return ConvGateHip32.apply(x.float(), weight_norm_effective(module), module.bias, cond,
+                                   module.dilation[0], module.padding[0], in_slope)
     t16 = _TORCH_16[wdt]
     w = weight_norm_effective(module)
     ent = _PREPACK.get(module)

@@ -25,7 +25,6 @@ callers keep torch's hooks on CPU.
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 from torch.nn.utils.spectral_norm import SpectralNorm
@@ -34,7 +33,7 @@ from torch.nn.utils.weight_norm import WeightNorm
 from . import _lib, ops
 from ._lib import SnormLayer, WnormLayer, check
 
-FUSED_NORMS = os.environ.get("VITS_FUSED_NORMS", "1") != "0"  # A/B switch (both)
+FUSED_NORMS = True  # test switch (both norms)
 FUSED_WN = FUSED_SN = True  # per-kind switches (diagnostics)
 
 
