@@ -230,7 +230,9 @@ def _ddp_worker(rank, world, port, out_dir, mode="ddp"):
     hps = tiny_hps()
     # different init per rank: the allreduce mode must broadcast rank 0's
     st = _make(hps, torch.device("cpu"), ddp=mode == "ddp", seed=0 if mode == "ddp" else rank,
-               allreduce=mode == "allreduce")
+               allreduce={"allreduce": True, "flat": "flat"}.get(mode, False))
+    if mode == "allreduce":  # G's gradients go through the overlapped buckets
+        assert st._gbuckets is not None and len(st._gbuckets.buckets) >= 3
     for i in range(2):
         out = st.step(_batch(hps, 2, seed=10 * i + rank))  # different data per rank
     flat = torch.cat([p.detach().flatten() for p in st.net_g.parameters()] +
@@ -281,10 +283,11 @@ def test_capture_failure_on_one_rank_falls_back_on_all_ranks(tmp_path):
     assert np.array_equal(np.load(tmp_path / "rank0.npy"), np.load(tmp_path / "rank1.npy"))
 
 
-@pytest.mark.parametrize("mode", ["ddp", "allreduce"])
+@pytest.mark.parametrize("mode", ["ddp", "allreduce", "flat"])
 def test_ddp_gloo_world2_replicas_stay_identical(tmp_path, mode):
-    """Both multi-process modes (DDP; the graph-capturable flat all-reduce)
-    keep the replicas bit-identical while each rank sees different data."""
+    """Every multi-process mode (DDP; the graph-capturable all-reduce with
+    G's gradients in overlapped buckets; the same with one flat all-reduce)
+    keeps the replicas bit-identical while each rank sees different data."""
     port = _free_port()
     mp.spawn(_ddp_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
     a = np.load(tmp_path / "rank0.npy")
@@ -292,6 +295,19 @@ def test_ddp_gloo_world2_replicas_stay_identical(tmp_path, mode):
     assert np.array_equal(a, b)  # gradient all-reduce -> identical updates
     la, lb = np.load(tmp_path / "loss0.npy"), np.load(tmp_path / "loss1.npy")
     assert np.isfinite(la).all() and np.isfinite(lb).all() and la[0] != lb[0]
+
+
+def test_bucketed_allreduce_equals_flat_allreduce(tmp_path):
+    """The overlapped bucketed G all-reduce averages exactly what the flat
+    one does: two steps of each mode from the same seeds and data end in
+    bit-identical parameters."""
+    res = {}
+    for mode in ("allreduce", "flat"):
+        d = tmp_path / mode
+        d.mkdir()
+        mp.spawn(_ddp_worker, args=(2, _free_port(), str(d), mode), nprocs=2, join=True)
+        res[mode] = np.load(d / "rank0.npy")
+    assert np.array_equal(res["allreduce"], res["flat"])
 
 
 @pytest.mark.gpu
@@ -477,3 +493,36 @@ def test_train_step_mel_variant_base_config_eager(device):
         assert torch.isfinite(out["loss_disc"])
     assert any(not torch.equal(a, b) for a, b in zip(g0, net_g.parameters()))
     assert any(not torch.equal(a, b) for a, b in zip(d0, net_d.parameters()))
+
+
+@pytest.mark.gpu
+def test_bucketed_rccl_allreduce_in_captured_step(device):
+    """The overlapped bucketed G all-reduce inside a captured hipGraph on
+    RCCL (a one-rank nccl group on this GPU: the side stream, its event fork
+    / join and the RCCL kernels are all captured and replayed): replays stay
+    finite and end bit-identical to the flat all-reduce's capture (one rank:
+    both are the identity on the gradients)."""
+    hps = tiny_hps()
+    hps.train.fp16_run = False  # fp32: no fp16 rounding chaos between the two runs
+    batch = [t.to(device) for t in _batch(hps, 4, seed=0)]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1)
+    old_det = torch.backends.cudnn.deterministic
+    # (MIOpen's default find picks run-dependent solvers for the STFT
+    # discriminators' convs: profiles/r05_determinism.txt)
+    torch.backends.cudnn.deterministic = True
+    try:
+        res = {}
+        for mode in (True, "flat"):
+            st = _make(hps, device, seed=0, capturable=True, allreduce=mode)
+            assert (st._gbuckets is not None) == (mode is True)
+            st.capture(batch, warmup=2)
+            for _ in range(2):
+                out = st.replay()
+            torch.cuda.synchronize()
+            assert torch.isfinite(out["loss_gen_all"]) and torch.isfinite(out["loss_disc"])
+            res[mode] = torch.cat([p.detach().flatten() for p in st.net_g.parameters()])
+        assert torch.equal(res[True], res["flat"])
+    finally:
+        torch.backends.cudnn.deterministic = old_det
+        dist.destroy_process_group()

@@ -56,14 +56,105 @@ def build_models(hps, device, variant: str = "stft"):
     return net_g, net_d
 
 
+# G's gradient buckets for the overlapped all-reduce, by parameter-name
+# prefix, in the order the backward finishes them: the decoder's gradients
+# are final first (its backward runs first, and its weight-norm group's
+# backward fires as soon as its last conv's weight gradient is in), then the
+# flow's, the posterior encoder's, and the rest (text encoder, duration
+# predictor, embeddings) last
+G_BUCKETS = ("dec.", "flow.", "enc_q.", "")
+
+
+class _GradBuckets:
+    """Bucketed, overlapped gradient all-reduce for one network (the
+    graph-capturable counterpart of DDP's reducer, train_stft.py:108-110):
+    each parameter's post-accumulate-grad hook counts its bucket down, and a
+    bucket whose gradients are all final is averaged over the ranks at once
+    - on the GPU on a side stream (forked from the backward's stream by an
+    event: copy into one flat buffer, one RCCL all-reduce over xGMI, scale,
+    copy back) while the backward of the earlier layers continues; on CPU
+    (gloo) synchronously.  finish() launches any bucket still waiting (a
+    parameter without a gradient this step) and joins the side stream."""
+
+    def __init__(self, net, prefixes, device):
+        self.device = device
+        named = [(n, p) for n, p in net.named_parameters() if p.requires_grad]
+        self.buckets = [[] for _ in prefixes]
+        for n, p in named:
+            i = next(i for i, pre in enumerate(prefixes) if n.startswith(pre))
+            self.buckets[i].append(p)
+        self.buckets = [b for b in self.buckets if b]
+        self.comm = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self._flat = {}
+        self._left = None
+        self._hooks = []
+        for bi, ps in enumerate(self.buckets):
+            for p in ps:
+                self._hooks.append(p.register_post_accumulate_grad_hook(
+                    lambda p, bi=bi: self._arrived(bi)))
+
+    def begin(self):
+        self._left = [len(b) for b in self.buckets]
+        self._done = [False] * len(self.buckets)
+
+    def _arrived(self, bi):
+        if self._left is None:  # (a backward outside step(): no all-reduce)
+            return
+        self._left[bi] -= 1
+        if self._left[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        self._done[bi] = True
+        ps = [p for p in self.buckets[bi] if p.grad is not None]
+        if not ps:
+            return
+        key = tuple(id(p) for p in ps)
+        ent = self._flat.get((bi, key))
+        if ent is None:
+            flat = torch.empty(sum(p.numel() for p in ps), device=ps[0].device,
+                               dtype=torch.float32)
+            views, o = [], 0
+            for p in ps:
+                views.append(flat[o:o + p.numel()].view_as(p))
+                o += p.numel()
+            ent = (flat, views)
+            self._flat[(bi, key)] = ent
+        flat, views = ent
+        grads = [p.grad for p in ps]
+        if self.comm is None:
+            torch._foreach_copy_(views, grads)
+            dist.all_reduce(flat)
+            flat.div_(dist.get_world_size())
+            torch._foreach_copy_(grads, views)
+            return
+        main = torch.cuda.current_stream(self.device)
+        self.comm.wait_stream(main)  # this bucket's gradients are final on `main`
+        with torch.cuda.stream(self.comm):
+            torch._foreach_copy_(views, grads)
+            dist.all_reduce(flat)
+            flat.div_(dist.get_world_size())
+            torch._foreach_copy_(grads, views)
+
+    def finish(self):
+        for bi, done in enumerate(self._done):
+            if not done:
+                self._launch(bi)
+        self._left = None
+        if self.comm is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm)
+
+
 class TrainStep:
     def __init__(self, hps, net_g, net_d, device, ddp=False, log_mels=True, fused_adamw=True,
                  capturable=False, allreduce=False, variant: str = "stft"):
         """ddp: wrap both networks in DDP (eager steps).  allreduce: the
         graph-capturable alternative for multi-process runs - no DDP hooks;
-        rank 0's parameters/buffers are broadcast once and each network's
-        gradients are averaged after its backward with one flat RCCL
-        all-reduce (the same averaged-gradient semantics as DDP)."""
+        rank 0's parameters/buffers are broadcast once, G's gradients are
+        averaged in buckets that overlap its backward (_GradBuckets,
+        G_BUCKETS; allreduce="flat": one flat all-reduce after the
+        backward) and D's with one flat RCCL all-reduce after its backward
+        (the same averaged-gradient semantics as DDP)."""
         assert not (ddp and allreduce)
         assert variant in ("stft", "mel"), variant
         # "stft": train_stft.py (MWSD D + MR-STFT loss, D optimizer RAdam);
@@ -119,6 +210,8 @@ class TrainStep:
             net_d = DDP(net_d, device_ids=ids)
         self.allreduce = bool(allreduce) and dist.is_available() and dist.is_initialized()
         self._flat = {}
+        self._gbuckets = (_GradBuckets(net_g, G_BUCKETS, device)
+                          if self.allreduce and allreduce != "flat" else None)
         if self.allreduce:
             with torch.no_grad():
                 for net in (net_g, net_d):
@@ -126,7 +219,8 @@ class TrainStep:
                         dist.broadcast(t, src=0)
         self.net_g, self.net_d = net_g, net_d
         # every weight-normed generator layer in one launch each way (GPU)
-        self._wn_g = (WeightNormCache(net_g.module if isinstance(net_g, DDP) else net_g)
+        self._wn_g = (WeightNormCache(net_g.module if isinstance(net_g, DDP) else net_g,
+                                      G_BUCKETS if self._gbuckets is not None else ("",))
                       if device.type == "cuda" else None)
         fp16 = bool(hps.train.fp16_run) and device.type == "cuda"
         # the autocast weight-cast cache must be off under graph capture (cached
@@ -210,10 +304,7 @@ class TrainStep:
                 loss_gen, _ = generator_loss(y_d_hat_g)
                 loss_gen_all = loss_gen + loss_stft + loss_dur + loss_kl + loss_kl_q
         with rf("step:G.backward"):
-            self.optim_g.zero_grad()
-            self.scaler.scale(loss_gen_all).backward()
-            if self.allreduce:
-                self._allreduce_grads("g", self.net_g)
+            self._backward_g(loss_gen_all)
         for p in d_params:
             p.requires_grad_(True)
         with rf("step:G.optimizer"):
@@ -287,10 +378,7 @@ class TrainStep:
                 loss_gen, _ = generator_loss(y_d_hat_g)
                 loss_gen_all = loss_gen + loss_fm + loss_mel + loss_dur + loss_kl + loss_kl_q
         with rf("step:G.backward"):
-            self.optim_g.zero_grad()
-            self.scaler.scale(loss_gen_all).backward()
-            if self.allreduce:
-                self._allreduce_grads("g", self.net_g)
+            self._backward_g(loss_gen_all)
         for p in d_params:
             p.requires_grad_(True)
         with rf("step:G.optimizer"):
@@ -303,6 +391,19 @@ class TrainStep:
                 "loss_mel": loss_mel.detach(), "loss_fm": loss_fm.detach(),
                 "loss_dur": loss_dur.detach(), "loss_kl": loss_kl.detach(),
                 "grad_norm_g": grad_norm_g, "grad_norm_d": grad_norm_d}
+
+    def _backward_g(self, loss_gen_all):
+        """G's scaled backward; under allreduce its gradients are averaged
+        over the ranks - bucket by bucket while the backward runs, or (flat
+        mode) in one all-reduce afterwards."""
+        self.optim_g.zero_grad()
+        if self._gbuckets is not None:
+            self._gbuckets.begin()
+        self.scaler.scale(loss_gen_all).backward()
+        if self._gbuckets is not None:
+            self._gbuckets.finish()
+        elif self.allreduce:
+            self._allreduce_grads("g", self.net_g)
 
     def _allreduce_grads(self, key, net):
         """Average this network's gradients over the ranks: one flat buffer,

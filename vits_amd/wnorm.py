@@ -113,9 +113,15 @@ class WeightNormCache:
     ``active()``, ``ops.weight_norm_effective(layer)`` returns the weight
     computed for all of them by one ``vits_weight_norm_forward`` launch."""
 
-    def __init__(self, root: torch.nn.Module):
+    def __init__(self, root: torch.nn.Module, groups=("",)):
+        """groups: module-name prefixes; each group's weights come from one
+        launch and go back in one (its backward runs as soon as that group's
+        last weight gradient is in: the decoder's long before the text
+        encoder's, so its gradients can be all-reduced while the rest of the
+        backward runs - train._GradBuckets)."""
         self.mods = []
-        for m in root.modules():
+        self.groups = [[] for _ in groups]
+        for name, m in root.named_modules():
             h = _weight_norm_hook(m)
             if h is None or h.dim != 0:
                 continue
@@ -123,12 +129,18 @@ class WeightNormCache:
             if g.dtype == v.dtype == torch.float32 and v.is_cuda and v.is_contiguous() \
                     and g.is_contiguous() and g.numel() == v.shape[0]:
                 self.mods.append((m, h.name))
+                gi = next(i for i, pre in enumerate(groups) if (name + ".").startswith(pre))
+                self.groups[gi].append((m, h.name))
+        self.groups = [grp for grp in self.groups if grp]
 
     def weights(self):
-        gs = [getattr(m, n + "_g") for m, n in self.mods]
-        vs = [getattr(m, n + "_v") for m, n in self.mods]
-        ws = _WeightNormAll.apply(len(self.mods), *gs, *vs)
-        return {m: w for (m, _), w in zip(self.mods, ws)}
+        out = {}
+        for grp in self.groups:
+            gs = [getattr(m, n + "_g") for m, n in grp]
+            vs = [getattr(m, n + "_v") for m, n in grp]
+            ws = _WeightNormAll.apply(len(grp), *gs, *vs)
+            out.update({m: w for (m, _), w in zip(grp, ws)})
+        return out
 
     @contextlib.contextmanager
     def active(self):
