@@ -265,7 +265,7 @@ def split_planes(w: torch.Tensor) -> torch.Tensor:
     (x - hi) truncated, lo = x - hi - mid (<= 8 significant bits), so
     hi + mid + lo == x bit for bit - conv1d_impl.h split3_bf16 on the host."""
     w = w.to(torch.float32).contiguous()
-    mask = torch.tensor(-65536, dtype=torch.int32, device=w.device)
+    mask = -65536  # (a Python scalar: no host-to-device copy, graph-capture safe)
     h = (w.view(torch.int32) & mask).view(torch.float32)
     # (a non-finite weight keeps mid = lo = 0: inf - inf would make them NaN;
     # a NaN stays NaN in hi even when its payload sits in the truncated bits)
