@@ -514,6 +514,15 @@ int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int ba
 /* the members share t_len and lengths; accumulate / post_div ignored.    */
 int vits_resblock_pair16_mean_forward(const vits_resblock_pair_desc* d, int n, int batch,
                                       int wdtype, void* stream);
+/* The same pair for the split-fp32 (VITS_WDT_F32P) 64-, 128- and 256-  */
+/* channel stages of an fp32 Generator (csrc/resblock_f32p.hip;           */
+/* modules.py:250-260): x / y fp32 [B][C][T], w1 / w2 the pre-split       */
+/* images [cin_pad/16][k][2][3][m_pad][8] bf16 of vits_conv1d_desc (w1's  */
+/* rows gate-interleaved); kc1 / kc2 ignored.  Bitwise the two-conv path  */
+/* (c1 with the gate epilogue, c2 with the residual one).  Odd k,         */
+/* (k - 1) * dil <= 96, T % 4 == 0, 16-byte aligned x rows.               */
+int vits_resblock_pair_f32p_forward(const vits_resblock_pair_desc* d, int n, int batch,
+                                    void* stream);
 
 /* Fused RAdam step (radam.py:35-99, the D optimizer of train_stft.py:97) */
 /* over a list of fp32 tensors, one launch per VITS_RADAM_MAX tensors.     */

@@ -586,6 +586,83 @@ def test_resblock_pair16_fused(device, C, k, dil, T, wdt):
     _close(mean, (refs[0] + refs[1] + refs[2]) / 3, tol=tol, what="mean launch")
 
 
+@pytest.mark.parametrize("C,k,dil,T", [
+    (64, 3, 1, 12), (64, 11, 5, 1000), (64, 7, 3, 2052), (128, 3, 5, 48), (128, 11, 5, 1000),
+    (128, 7, 1, 500), (256, 11, 3, 300), (256, 3, 1, 132),
+])
+def test_resblock_pair_f32p_fused(device, monkeypatch, C, k, dil, T):
+    """csrc/resblock_f32p.hip (the split-fp32 pair of the 64/128/256-channel
+    stages) equals the two-conv path it replaces BIT FOR BIT - c1 with the
+    gate epilogue into an fp32 gated tensor, c2 with the residual epilogue:
+    the same split planes, k-step order, products and epilogue expressions -
+    for the three-branch grouped launch, the branch-mean epilogue
+    (accumulate, post_div) and utterance lengths (the gated tensor and the
+    output zero past them); and matches the pair in fp64 to 2e-6 of the
+    output magnitude (fp32 arithmetic)."""
+    g = torch.Generator().manual_seed(C + k + dil + T)
+    B = 2
+    packs, refs, xs = [], [], []
+    # (the kernel takes every stage and k; the engine's rule picks where)
+    monkeypatch.setattr(ops, "F32P_PAIR_MAX_K", {64: 15, 128: 15, 256: 15})
+    for j in range(3):
+        x = torch.randn(B, C, T, generator=g) * 0.5
+        w1 = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
+        b1 = torch.randn(C, generator=g) * 0.1
+        w2 = torch.randn(C, C // 2, k, generator=g) / (C * k / 2) ** 0.5
+        b2 = torch.randn(C, generator=g) * 0.1
+        cond = torch.randn(B, C, generator=g) * 0.3
+        c1 = ops.to_lowp(ops.pack_conv(w1.to(device), b1.to(device), dilation=dil, gate=True),
+                         ops.WDT_F32S)
+        c2 = ops.to_lowp(ops.pack_conv(w2.to(device), b2.to(device)), ops.WDT_F32S)
+        assert c1.wdtype == c2.wdtype == ops.WDT_F32P
+        xd = x.to(device)
+        assert ops.resblock_pair_f32p_supported(c1, c2, xd)
+        packs.append((c1, c2, cond.to(device)))
+        refs.append(_resblock_pair_ref(x, w1, b1, cond, w2, b2, k, dil))
+        xs.append(xd)
+
+    def two_conv(j, y, lengths=None, **kw):
+        c1, c2, cd = packs[j]
+        gbuf = torch.full((B, C // 2, T), float("nan"), device=device)
+        ops.conv1d_launch_seq([
+            ops.make_desc(c1, xs[j], ops.make_out(gbuf), in_slope=0.1, cond=cd, lengths=lengths),
+            ops.make_desc(c2, gbuf, ops.make_out(y, res=xs[j], **kw), lengths=lengths)], B, device)
+
+    def fused(js, ys, lengths=None, **kw):
+        ops.resblock_pair_launch(tuple(
+            ops.resblock_pair_desc(packs[j][0], packs[j][1], xs[j], y, cond=packs[j][2],
+                                   lengths=lengths, **kw) for j, y in zip(js, ys)),
+            B, device, ops.WDT_F32P)
+
+    ys = [torch.full((B, C, T), float("nan"), device=device) for _ in range(3)]
+    fused(range(3), ys)
+    for j in range(3):
+        y2 = torch.full((B, C, T), float("nan"), device=device)
+        two_conv(j, y2)
+        torch.cuda.synchronize()
+        d = (ys[j] - y2).abs().max().item()
+        assert torch.equal(ys[j], y2), f"pair {j}: fused != two-conv, max diff {d:.3e}"
+        _close(ys[j], refs[j], tol=2e-6, what=f"pair {j} vs fp64")
+    # branch mean: accumulate in branch order, the last divides
+    acc, acc2 = torch.empty(B, C, T, device=device), torch.empty(B, C, T, device=device)
+    for j in range(3):
+        kw = dict(accumulate=j > 0, post_div=3.0 if j == 2 else 1.0)
+        fused([j], [acc], **kw)
+        two_conv(j, acc2, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(acc, acc2), "mean"
+    _close(acc, (refs[0] + refs[1] + refs[2]) / 3, tol=2e-6, what="mean vs fp64")
+    # utterance lengths (bucketed inference): zero past them, bitwise again
+    lens = torch.tensor([T, max(1, T - 37)], dtype=torch.int32, device=device)
+    yl = [torch.zeros(B, C, T, device=device) for _ in range(3)]
+    fused(range(3), yl, lengths=lens)
+    for j in range(3):
+        y2 = torch.zeros(B, C, T, device=device)
+        two_conv(j, y2, lengths=lens)
+        torch.cuda.synchronize()
+        assert torch.equal(yl[j], y2), f"pair {j} with lengths"
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_generator16_fused_pairs_match_two_conv_path(device, monkeypatch, dt):
     """A 16-bit model's Generator with resblock16 pairs on its 32/64-channel

@@ -324,6 +324,8 @@ _SIGS = {
     ),
     "vits_resblock_pair_forward": (
         C.c_int, [C.POINTER(ResblockPairDesc), C.c_int, C.c_int, C.c_void_p]),
+    "vits_resblock_pair_f32p_forward": (
+        C.c_int, [C.POINTER(ResblockPairDesc), C.c_int, C.c_int, C.c_void_p]),
     "vits_resblock_pair_kc": (
         C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vits_resblock_pair16_forward": (

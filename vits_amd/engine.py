@@ -237,7 +237,8 @@ class GeneratorPlan:
         def can_fuse(pr):
             if io16:  # 16-bit model, 16-bit activations: csrc/resblock16.hip
                 return ops.resblock_pair16_supported(pr[0], pr[1], xu)
-            return _FUSED_PAIRS and ops.resblock_pair_supported(pr[0], pr[1], T)
+            return _FUSED_PAIRS and (ops.resblock_pair_supported(pr[0], pr[1], T) or
+                                     ops.resblock_pair_f32p_supported(pr[0], pr[1], xu))
 
         fused = [[can_fuse(pr) for pr in pairs] for pairs in blocks]
 
@@ -250,7 +251,7 @@ class GeneratorPlan:
             if io16:
                 ops.resblock_pair16_launch(descs, B, dev, blocks[0][0][0].wdtype)
             else:
-                ops.resblock_pair_launch(descs, B, dev)
+                ops.resblock_pair_launch(descs, B, dev, blocks[0][0][0].wdtype)
         tmp = [[torch.empty_like(xs), torch.empty_like(xs)] for _ in range(nk)]
         gbuf = [None if all(fused[j]) else
                 torch.empty(B, C // 2, T, device=dev, dtype=xu.dtype) for j in range(nk)]

@@ -578,13 +578,17 @@ class ConvTimer:
         if wdtype is None:
             check(lib.vits_resblock_pair_forward(arr, len(group), batch, stream.cuda_stream),
                   "vits_resblock_pair_forward")
+        elif wdtype == WDT_F32P:
+            check(lib.vits_resblock_pair_f32p_forward(arr, len(group), batch, stream.cuda_stream),
+                  "vits_resblock_pair_f32p_forward")
         else:
             fn = lib.vits_resblock_pair16_mean_forward if mean else lib.vits_resblock_pair16_forward
             check(fn(arr, len(group), batch, int(wdtype), stream.cuda_stream),
                   "vits_resblock_pair16_forward")
         e.record(stream)
         self.records.append((s, e, sum(resblock_pair_flops(d, batch) for d in group)))
-        self.peaks.append(MFMA_PEAK_TFLOPS[WDT_F32 if wdtype is None else wdtype])
+        self.peaks.append(MFMA_PEAK_TFLOPS[WDT_F32 if wdtype is None else
+                                           WDT_F32S if wdtype == WDT_F32P else wdtype])
         self.shapes.append("pair " + "+".join(
             f"C{d.channels}k{d.k}d{d.dil}T{d.t_len}" for d in group))
 
@@ -630,6 +634,30 @@ def resblock_pair_supported(c1: PackedConv, c2: PackedConv, T: int) -> bool:
             and _resblock_kc(C, c1.k, c1.dil) is not None)
 
 
+# split-fp32 fused pairs (csrc/resblock_f32p.hip): channels -> largest k that
+# runs fused.  tools/rbp_bench.py on MI355X (B=16, Ty=500, each branch alone,
+# profiles/r05_rbp_bench.txt): C=64 fused vs two-conv k=3 -23 %, k=7 -12 %,
+# k=11 -2 %; C=128 k=3 -25 %, k=7 -4..-8 %, k=11 +-0 (the c1 phase
+# recomputes c2's halo: 10 of 128 columns at k=11); C=256 (64-column tiles,
+# every workgroup streams the whole c1 weight image) k=3 -2 %, k=7 / k=11
+# +8..15 % - so 256 keeps the two-conv path
+F32P_PAIR_MAX_K = {64: 11, 128: 7}
+
+
+def resblock_pair_f32p_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -> bool:
+    """Pairs of an fp32 Generator's split-fp32 stages (pre-split images,
+    VITS_WDT_F32P) that run fused (csrc/resblock_f32p.hip): odd k, 'same'
+    padding, (k - 1) * dil <= 96, 16-byte aligned fp32 time rows."""
+    C_ = c2.out_channels
+    return (c1.wdtype == WDT_F32P and c2.wdtype == WDT_F32P and c1.k <= F32P_PAIR_MAX_K.get(C_, 0)
+            and x.dtype == torch.float32 and c1.m == C_ and c1.cin == C_ and c2.cin == C_ // 2
+            and c2.m == C_ and c1.k == c2.k and c1.k % 2 == 1 and (c1.k - 1) * c1.dil <= 96
+            and c2.dil == 1 and c1.epi == EPI_GATE and c2.epi == EPI_STORE
+            and c1.pad_left == (c1.k - 1) * c1.dil // 2 and c2.pad_left == (c2.k - 1) // 2
+            and x.shape[2] % 4 == 0 and x.stride(2) == 1 and x.stride(1) % 4 == 0
+            and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
+
+
 def _resblock_kc(ch: int, k: int, dil: int):
     key = (ch, k, dil)
     if key not in _RB_KC:
@@ -648,7 +676,8 @@ def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch
     ``lengths`` (int32 [B], device): the utterance ends there (zero past)."""
     assert x.dtype == torch.float32 and y.dtype == torch.float32 and x.stride(2) == 1
     C_, T = x.shape[1], x.shape[2]
-    kc1, kc2 = _resblock_kc(C_, c1.k, c1.dil)
+    # (the split-fp32 kernel stages 16-channel slabs: no kc choice)
+    kc1, kc2 = (16, 16) if c1.wdtype == WDT_F32P else _resblock_kc(C_, c1.k, c1.dil)
     d = ResblockPairDesc()
     d.x, d.x_bstride, d.x_cstride, d.t_len = x.data_ptr(), x.stride(0), x.stride(1), T
     d.channels, d.in_slope = C_, in_slope
@@ -730,13 +759,20 @@ def resblock_pair_flops(d: ResblockPairDesc, batch: int) -> int:
     return 2 * batch * T * (C_ * C_ * k + (C_ // 2) * C_ * k)
 
 
-def resblock_pair_launch(descs, batch: int, device: torch.device):
-    """One launch of up to 3 independent pairs (tuple) or one pair."""
+def resblock_pair_launch(descs, batch: int, device: torch.device, wdtype: int = WDT_F32):
+    """One launch of up to 3 independent pairs (tuple) or one pair; wdtype
+    WDT_F32 (exact fp32, csrc/resblock.hip) or WDT_F32P (split fp32,
+    csrc/resblock_f32p.hip)."""
     group = tuple(descs) if isinstance(descs, (tuple, list)) else (descs,)
     lib = _lib.load()
     if ConvTimer.active is not None:
-        return ConvTimer.active.launch_pairs(lib, group, batch, device)
+        return ConvTimer.active.launch_pairs(lib, group, batch, device,
+                                             wdtype=WDT_F32P if wdtype == WDT_F32P else None)
     arr = (ResblockPairDesc * len(group))(*group)
+    if wdtype == WDT_F32P:
+        check(lib.vits_resblock_pair_f32p_forward(arr, len(group), batch, _stream_ptr(device)),
+              "vits_resblock_pair_f32p_forward")
+        return
     check(lib.vits_resblock_pair_forward(arr, len(group), batch, _stream_ptr(device)),
           "vits_resblock_pair_forward")
 
