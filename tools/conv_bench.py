@@ -28,6 +28,8 @@ CHECK = os.environ.get("CHECK", "0") == "1"  # error vs the exact-f32 kernel and
 tiles = [int(t) for t in os.environ.get("TILES", "").split(",") if t]
 kcms = [int(t) for t in os.environ.get("KCM", "1").split(",") if t]
 reps = int(os.environ.get("REPS", "5"))
+if os.environ.get("F32P_KC"):  # chunk channels of the split-fp32 128-row tiles (32 / 16)
+    ops.F32P_MAX_KC = int(os.environ["F32P_KC"])
 tot_fl, tot_ms = 0, 0
 res = {}
 for name, cin, cout, k, d, T, gate, up in shapes:

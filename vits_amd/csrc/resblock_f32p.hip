@@ -32,8 +32,9 @@
 // the same k-step order (slab-major, then tap), the same six products per
 // fragment pair in the same order, the same gate and epilogue expressions
 // (tests/test_resblock_f32p_gpu.py checks equality).  Tiles: C = 64 ->
-// 64 x 256 (1 x 4 waves), C = 128 -> 128 x 128 (2 x 2), C = 256 -> 256 x 64
-// (4 x 1); two workgroups per CU.  Every launch holds up to 3 independent
+// 64 x 256 (1 x 4 waves), C = 128 -> 128 x 128 (2 x 2), two workgroups per
+// CU; C = 256 -> 256 x 128 (4 x 2 waves, one 512-thread workgroup per CU:
+// the same two waves per SIMD).  Every launch holds up to 3 independent
 // pairs (the branches of a stage).
 #include "conv1d_impl.h"
 
@@ -56,7 +57,9 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-__host__ __device__ constexpr int rp_ng(int C) { return C == 64 ? 256 : C == 128 ? 128 : 64; }
+__host__ __device__ constexpr int rp_ng(int C) { return C == 64 ? 256 : 128; }
+// threads: 4 waves (C = 64, 128), 8 waves of 64 x 64 (C = 256: 256 x 128)
+__host__ __device__ constexpr int rp_threads(int C) { return C == 256 ? 512 : 256; }
 __host__ __device__ inline int rp_xcols(int NG, int k, int dil) {
   // NG + (k-1) dil window columns + up to 3 of alignment shift, 4-blocks
   return ((NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
@@ -70,10 +73,12 @@ __host__ __device__ inline int rp_lds_bytes(int C, int k, int dil) {
 }
 
 template <int C>
-__global__ __launch_bounds__(256, 2) void resblock_f32p_kernel(const RpGroup G) {
+__global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f32p_kernel(
+    const RpGroup G) {
   constexpr int H = C / 2;
+  constexpr int NT = rp_threads(C);
   constexpr int WAVES_M = C / 64;
-  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WAVES_N = NT / 64 / WAVES_M;
   constexpr int NG = 64 * WAVES_N;
   static_assert(NG == rp_ng(C), "tile columns");
   constexpr int TM = 2, TN = 2;  // 64 x 64 per wave
@@ -81,7 +86,7 @@ __global__ __launch_bounds__(256, 2) void resblock_f32p_kernel(const RpGroup G) 
   constexpr int GP = H + 8;              // G row pitch (bf16): 16-byte rows
   constexpr int GPL = (NG + 16) * GP;    // G plane (elements)
   constexpr int S1 = C / 16, S2 = H / 16;
-  constexpr int NU = (NG + 102 + 255) / 256;  // staging units per thread (xcols <= NG + 102)
+  constexpr int NU = (NG + 102 + NT - 1) / NT;  // staging units per thread (xcols <= NG + 102)
   typedef bf16x8 av_t;
 
   const int gi = (int)blockIdx.z / G.batch;
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(256, 2) void resblock_f32p_kernel(const RpGroup G) 
 
   {
     const float* cond = p.cond ? p.cond + (int64_t)b * p.cond_bstride : nullptr;
-    for (int r = tid; r < 2 * C; r += 256) {
+    for (int r = tid; r < 2 * C; r += NT) {
       float e = 0.f;
       if (r < C) {
         const int idx = (r & 1) ? H + (r >> 1) : (r >> 1);
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(256, 2) void resblock_f32p_kernel(const RpGroup G) 
     bool xok[NU];
 #pragma unroll
     for (int q = 0; q < NU; ++q) {
-      const int u = tid + 256 * q;
+      const int u = tid + NT * q;
       const int tt = xstart + 4 * (u >> 2);
       xok[q] = u < nunits && tt >= 0 && tt < Tn;  // T % 4 == 0: a block is all in or out
       xoff[q] = xok[q] ? 4 * (u & 3) * p.x_cstride + tt : 0;
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void resblock_f32p_kernel(const RpGroup G) 
       const float* base = xb + (int64_t)sl * 16 * p.x_cstride;
 #pragma unroll
       for (int q = 0; q < NU; ++q) {
-        if (q * 256 < nunits) {
+        if (q * NT < nunits) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float* src = xok[q] ? base + xoff[q] + i * p.x_cstride : xb;
@@ -206,8 +211,8 @@ __global__ __launch_bounds__(256, 2) void resblock_f32p_kernel(const RpGroup G) 
     auto lstore = [&](__bf16* xs) {
 #pragma unroll
       for (int q = 0; q < NU; ++q) {
-        const int u = tid + 256 * q;
-        if (q * 256 < nunits && u < nunits) {
+        const int u = tid + NT * q;
+        if (q * NT < nunits && u < nunits) {
           f32x4v v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(256, 2) void resblock_f32p_kernel(const RpGroup G) 
     }
   }
   // the 16 rows past NG that phase 2's discarded columns read: zero
-  for (int i = tid; i < 3 * 16 * H; i += 256) {
+  for (int i = tid; i < 3 * 16 * H; i += NT) {
     const int pl = i / (16 * H);
     const int e = i - pl * 16 * H;
     gs[pl * GPL + (NG + e / H) * GP + e % H] = (__bf16)0.f;
@@ -412,7 +417,8 @@ int rp_launch(const RpGroup& g, hipStream_t s) {
     if (x > gx) gx = x;
   }
   if (lds > 160 * 1024) return VITS_E_UNSUP;
-  hipLaunchKernelGGL((resblock_f32p_kernel<C>), dim3(gx, 1, g.n * g.batch), dim3(256), lds, s, g);
+  hipLaunchKernelGGL((resblock_f32p_kernel<C>), dim3(gx, 1, g.n * g.batch), dim3(rp_threads(C)), lds,
+                     s, g);
   return vits_launch_status();
 }
 

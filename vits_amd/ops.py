@@ -636,12 +636,12 @@ def resblock_pair_supported(c1: PackedConv, c2: PackedConv, T: int) -> bool:
 
 # split-fp32 fused pairs (csrc/resblock_f32p.hip): channels -> largest k that
 # runs fused.  tools/rbp_bench.py on MI355X (B=16, Ty=500, each branch alone,
-# profiles/r05_rbp_bench.txt): C=64 fused vs two-conv k=3 -23 %, k=7 -12 %,
+# profiles/r05_rbp_bench*.txt): C=64 fused vs two-conv k=3 -23 %, k=7 -12 %,
 # k=11 -2 %; C=128 k=3 -25 %, k=7 -4..-8 %, k=11 +-0 (the c1 phase
-# recomputes c2's halo: 10 of 128 columns at k=11); C=256 (64-column tiles,
-# every workgroup streams the whole c1 weight image) k=3 -2 %, k=7 / k=11
-# +8..15 % - so 256 keeps the two-conv path
-F32P_PAIR_MAX_K = {64: 11, 128: 7}
+# recomputes c2's halo: 10 of 128 columns at k=11); C=256 (one 512-thread
+# workgroup per CU, 543 tiles per utterance batch: 2.1 rounds of the chip)
+# k=3 -17 %, k=7 / k=11 +30..40 %
+F32P_PAIR_MAX_K = {64: 11, 128: 7, 256: 3}
 
 
 def resblock_pair_f32p_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -> bool:
