@@ -18,7 +18,7 @@
 //            each side; rows gate-interleaved), exactly the conv kernel's
 //            global-A loop: A fragments (hi / mid / lo planes) from the
 //            host-split image in L2, one k-step ahead; the x window staged
-//            one 16-channel slab at a time (lrelu, zero padding, exact
+//            16 channels (C = 256: 64) at a time (lrelu, zero padding, exact
 //            three-way bf16 split) into double-buffered [t][16 + 4] planes;
 //   gate:    tanh * sigmoid of the fp32 accumulators, split exactly into
 //            three bf16 planes G[t][C/2 + 8] in LDS (zero outside [0, L):
@@ -45,7 +45,6 @@ using vits_conv::fast_tanh;
 using vits_conv::split3_bf16x4;
 
 constexpr int RP_GROUP = 3;
-constexpr int RP_KCP = 20;  // X chunk row pitch (16 channels + 4, bf16)
 struct RpGroup {
   vits_resblock_pair_desc d[RP_GROUP];
   int n;
@@ -60,6 +59,11 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 __host__ __device__ constexpr int rp_ng(int C) { return C == 64 ? 256 : 128; }
 // threads: 4 waves (C = 64, 128), 8 waves of 64 x 64 (C = 256: 256 x 128)
 __host__ __device__ constexpr int rp_threads(int C) { return C == 256 ? 512 : 256; }
+// c1 channels per staged X chunk (one barrier each): 16 where two workgroups
+// share a CU (the double-buffered chunk must fit beside nothing but the G
+// planes it aliases), 64 for the one-workgroup 256-channel tile (its X
+// buffers still fit the LDS: four slabs per barrier)
+__host__ __device__ constexpr int rp_kc(int C) { return C == 256 ? 64 : 16; }
 __host__ __device__ inline int rp_xcols(int NG, int k, int dil) {
   // NG + (k-1) dil window columns + up to 3 of alignment shift, 4-blocks
   return ((NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
@@ -67,7 +71,7 @@ __host__ __device__ inline int rp_xcols(int NG, int k, int dil) {
 // LDS: erow [2C] floats, then max(two X slab buffers, the G planes)
 __host__ __device__ inline int rp_lds_bytes(int C, int k, int dil) {
   const int NG = rp_ng(C);
-  const int xs = 2 * 3 * rp_xcols(NG, k, dil) * RP_KCP;
+  const int xs = 2 * 3 * rp_xcols(NG, k, dil) * (rp_kc(C) + 4);
   const int gsz = 3 * (NG + 16) * (C / 2 + 8);
   return 4 * 2 * C + 2 * (xs > gsz ? xs : gsz) + 64;
 }
@@ -82,11 +86,12 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
   constexpr int NG = 64 * WAVES_N;
   static_assert(NG == rp_ng(C), "tile columns");
   constexpr int TM = 2, TN = 2;  // 64 x 64 per wave
-  constexpr int KCP = RP_KCP;
+  constexpr int KC = rp_kc(C);          // c1 channels per staged chunk
+  constexpr int KCP = KC + 4;           // X chunk row pitch (bf16)
   constexpr int GP = H + 8;              // G row pitch (bf16): 16-byte rows
   constexpr int GPL = (NG + 16) * GP;    // G plane (elements)
   constexpr int S1 = C / 16, S2 = H / 16;
-  constexpr int NU = (NG + 102 + NT - 1) / NT;  // staging units per thread (xcols <= NG + 102)
+  constexpr int NU = ((KC / 4) * ((NG + 102) / 4) + NT - 1) / NT;  // staging units per thread
   typedef bf16x8 av_t;
 
   const int gi = (int)blockIdx.z / G.batch;
@@ -177,26 +182,26 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
     const int xstart = tw0 & ~3;   // 16-byte aligned block start
     const int xsh = tw0 - xstart;  // window column c sits at LDS row c + xsh
     const int xcols = rp_xcols(NG, k, dil);
-    const int nunits = xcols;      // 4 channel quads x xcols / 4 blocks
+    const int nunits = (KC / 4) * (xcols >> 2);  // channel quads x 4-step blocks
     const int xpl = xcols * KCP;   // plane (elements)
     __bf16* const xbuf0 = reg;
     __bf16* const xbuf1 = reg + 3 * xpl;
     const float slope = p.in_slope;
-    // unit u: channel quad u & 3, 4-step block u >> 2 (a 16-lane group's
-    // 8-byte LDS pieces fall on distinct banks)
+    // unit u: channel quad u % (KC/4), 4-step block u / (KC/4) (a 16-lane
+    // group's 8-byte LDS pieces fall on distinct banks)
     f32x4v xr[NU][4];
     int xoff[NU];
     bool xok[NU];
 #pragma unroll
     for (int q = 0; q < NU; ++q) {
       const int u = tid + NT * q;
-      const int tt = xstart + 4 * (u >> 2);
+      const int tt = xstart + 4 * (u / (KC / 4));
       xok[q] = u < nunits && tt >= 0 && tt < Tn;  // T % 4 == 0: a block is all in or out
-      xoff[q] = xok[q] ? 4 * (u & 3) * p.x_cstride + tt : 0;
+      xoff[q] = xok[q] ? 4 * (u % (KC / 4)) * p.x_cstride + tt : 0;
     }
     // loads issued unconditionally (clamped address, zeroed in lstore)
-    auto gload = [&](int sl) {
-      const float* base = xb + (int64_t)sl * 16 * p.x_cstride;
+    auto gload = [&](int ch) {
+      const float* base = xb + (int64_t)ch * KC * p.x_cstride;
 #pragma unroll
       for (int q = 0; q < NU; ++q) {
         if (q * NT < nunits) {
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
               t = t < 0.f ? t * slope : t;
               v[i][e] = xok[q] ? t : 0.f;
             }
-          __bf16* xh = xs + 4 * (u >> 2) * KCP + 4 * (u & 3);
+          __bf16* xh = xs + 4 * (u / (KC / 4)) * KCP + 4 * (u % (KC / 4));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const f32x4v w = {v[0][e], v[1][e], v[2][e], v[3][e]};
@@ -235,14 +240,14 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
         }
       }
     };
-    // B fragments of tap j: rows wn + ni * 32 + l32 + j * dil (+ xsh),
-    // channels 8 lhi .. + 8 of the slab (two 8-byte reads per plane)
-    auto loadB = [&](const __bf16* xs, int j, av_t* bh, av_t* bm, av_t* bl) {
+    // B fragments of tap j, slab g of the chunk: rows wn + ni * 32 + l32 +
+    // j * dil (+ xsh), channels 16 g + 8 lhi .. + 8 (two 8-byte reads per plane)
+    auto loadB = [&](const __bf16* xs, int j, int g, av_t* bh, av_t* bm, av_t* bl) {
       const int P4 = xpl / 4;
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const bf16x4* xp = reinterpret_cast<const bf16x4*>(
-            xs + (wn + ni * 32 + l32 + j * dil + xsh) * KCP + 8 * lhi);
+            xs + (wn + ni * 32 + l32 + j * dil + xsh) * KCP + 16 * g + 8 * lhi);
         bh[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
         bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
         bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
@@ -252,32 +257,42 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
                        ((int64_t)(lhi * 3) * p.m_pad1 + wm + l32) * 8;
     const int64_t wstep = (int64_t)48 * p.m_pad1;
     const int total = S1 * k;
+    const int nst = (KC / 16) * k;  // k-steps per chunk: slab-major, then tap
     loadA(wl, wstep, p.m_pad1, 0, total, a0);
     gload(0);
     lstore(xbuf0);
     __syncthreads();
-    for (int sl = 0; sl < S1; ++sl) {
-      const bool more = sl + 1 < S1;
-      if (more) gload(sl + 1);  // in flight under this slab's MFMAs
-      const __bf16* xs = (sl & 1) ? xbuf1 : xbuf0;
-      const int s0 = sl * k;
-      loadB(xs, 0, bh0, bm0, bl0);
+    for (int ch = 0; ch < C / KC; ++ch) {
+      const bool more = ch + 1 < C / KC;
+      if (more) gload(ch + 1);  // in flight under this chunk's MFMAs
+      const __bf16* xs = (ch & 1) ? xbuf1 : xbuf0;
+      const int s0 = ch * nst;
+      int j = 0, g = 0;  // (tap, slab) of the next B load
+      auto next = [&]() {
+        if (++j == k) {
+          j = 0;
+          ++g;
+        }
+      };
+      loadB(xs, 0, 0, bh0, bm0, bl0);
       int st = 0;
       // the loads of step st + 1 pinned ahead of step st's MFMAs
-      for (; st + 2 <= k; st += 2) {
+      for (; st + 2 <= nst; st += 2) {
+        next();
         loadA(wl, wstep, p.m_pad1, s0 + st + 1, total, a1);
-        loadB(xs, st + 1, bh1, bm1, bl1);
+        loadB(xs, j, g, bh1, bm1, bl1);
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, bh0, bm0, bl0);
         __builtin_amdgcn_sched_barrier(0);
+        next();
         loadA(wl, wstep, p.m_pad1, s0 + st + 2, total, a0);
-        if (st + 2 < k) loadB(xs, st + 2, bh0, bm0, bl0);
+        if (st + 2 < nst) loadB(xs, j, g, bh0, bm0, bl0);
         __builtin_amdgcn_sched_barrier(0);
         mma(a1, bh1, bm1, bl1);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (st < k) {  // (k odd: the last tap, and the next slab's A)
-        loadA(wl, wstep, p.m_pad1, s0 + k, total, a1);
+      if (st < nst) {  // odd step count: the last step, and the next chunk's A
+        loadA(wl, wstep, p.m_pad1, s0 + nst, total, a1);
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, bh0, bm0, bl0);
 #pragma unroll
@@ -285,7 +300,7 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
 #pragma unroll
           for (int mi = 0; mi < TM; ++mi) a0[q][mi] = a1[q][mi];
       }
-      if (more) lstore((sl & 1) ? xbuf0 : xbuf1);
+      if (more) lstore((ch & 1) ? xbuf0 : xbuf1);
       __syncthreads();
     }
   }

@@ -653,6 +653,7 @@ def resblock_pair_f32p_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor
             and x.dtype == torch.float32 and c1.m == C_ and c1.cin == C_ and c2.cin == C_ // 2
             and c2.m == C_ and c1.k == c2.k and c1.k % 2 == 1 and (c1.k - 1) * c1.dil <= 96
             and c2.dil == 1 and c1.epi == EPI_GATE and c2.epi == EPI_STORE
+            and (C_ != 256 or (c1.k - 1) * c1.dil <= 56)  # (its 64-channel X chunks' LDS)
             and c1.pad_left == (c1.k - 1) * c1.dil // 2 and c2.pad_left == (c2.k - 1) // 2
             and x.shape[2] % 4 == 0 and x.stride(2) == 1 and x.stride(1) % 4 == 0
             and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
