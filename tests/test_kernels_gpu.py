@@ -588,7 +588,7 @@ def test_resblock_pair16_fused(device, C, k, dil, T, wdt):
 
 @pytest.mark.parametrize("C,k,dil,T", [
     (64, 3, 1, 12), (64, 11, 5, 1000), (64, 7, 3, 2052), (128, 3, 5, 48), (128, 11, 5, 1000),
-    (128, 7, 1, 500), (256, 11, 3, 300), (256, 3, 1, 132),
+    (128, 7, 1, 500), (256, 11, 3, 300), (256, 3, 1, 132), (32, 3, 1, 2000), (32, 11, 5, 600),
 ])
 def test_resblock_pair_f32p_fused(device, monkeypatch, C, k, dil, T):
     """csrc/resblock_f32p.hip (the split-fp32 pair of the 64/128/256-channel
@@ -603,7 +603,7 @@ def test_resblock_pair_f32p_fused(device, monkeypatch, C, k, dil, T):
     B = 2
     packs, refs, xs = [], [], []
     # (the kernel takes every stage and k; the engine's rule picks where)
-    monkeypatch.setattr(ops, "F32P_PAIR_MAX_K", {64: 15, 128: 15, 256: 15})
+    monkeypatch.setattr(ops, "F32P_PAIR_MAX_K", {32: 15, 64: 15, 128: 15, 256: 15})
     for j in range(3):
         x = torch.randn(B, C, T, generator=g) * 0.5
         w1 = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
@@ -612,8 +612,8 @@ def test_resblock_pair_f32p_fused(device, monkeypatch, C, k, dil, T):
         b2 = torch.randn(C, generator=g) * 0.1
         cond = torch.randn(B, C, generator=g) * 0.3
         c1 = ops.to_lowp(ops.pack_conv(w1.to(device), b1.to(device), dilation=dil, gate=True),
-                         ops.WDT_F32S)
-        c2 = ops.to_lowp(ops.pack_conv(w2.to(device), b2.to(device)), ops.WDT_F32S)
+                         ops.WDT_F32S, min_rows=0)
+        c2 = ops.to_lowp(ops.pack_conv(w2.to(device), b2.to(device)), ops.WDT_F32S, min_rows=0)
         assert c1.wdtype == c2.wdtype == ops.WDT_F32P
         xd = x.to(device)
         assert ops.resblock_pair_f32p_supported(c1, c2, xd)

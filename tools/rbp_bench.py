@@ -34,7 +34,7 @@ def timeit(fn):
 
 
 tot = {"two": 0.0, "fused": 0.0}
-for C, T in ((256, 8 * Ty), (128, 48 * Ty), (64, 96 * Ty)):
+for C, T in ((256, 8 * Ty), (128, 48 * Ty), (64, 96 * Ty), (32, 192 * Ty)):
     for d in (1, 3, 5):
         name = f"C{C}.d{d}"
         if only and only not in name:
@@ -46,8 +46,9 @@ for C, T in ((256, 8 * Ty), (128, 48 * Ty), (64, 96 * Ty)):
             w1 = torch.randn(C, C, k, device=dev) / (C * k) ** 0.5
             w2 = torch.randn(C, C // 2, k, device=dev) / (C * k / 2) ** 0.5
             c1 = ops.to_lowp(ops.pack_conv(w1, torch.zeros(C, device=dev), dilation=d, gate=True),
-                             ops.WDT_F32S)
-            c2 = ops.to_lowp(ops.pack_conv(w2, torch.zeros(C, device=dev)), ops.WDT_F32S)
+                             ops.WDT_F32S, min_rows=0)
+            c2 = ops.to_lowp(ops.pack_conv(w2, torch.zeros(C, device=dev)), ops.WDT_F32S,
+                             min_rows=0)
             gb = torch.empty(B, C // 2, T, device=dev)
             y = torch.empty(B, C, T, device=dev)
             d1 = make_desc(c1, x, make_out(gb), in_slope=0.1, cond=cond)
@@ -69,3 +70,35 @@ for C, T in ((256, 8 * Ty), (128, 48 * Ty), (64, 96 * Ty)):
             print(f"   k{k:<2d}  two-conv {a*1e3:7.1f} us {f1/a/1e9:6.1f} TF/s"
                   f"   fused {b*1e3:7.1f} us {f1/b/1e9:6.1f} TF/s", flush=True)
 print(f"TOTAL (groups) two-conv {tot['two']:.3f} ms  fused {tot['fused']:.3f} ms")
+# the 32-channel stage's shipped exact-fp32 path (resblock.hip pairs for k <= 7,
+# two exact convs for k = 11) beside the split-fp32 fused pair
+C, T = 32, 192 * Ty
+if not only or "C32" in only:
+    tex = tsp = 0.0
+    for d in (1, 3, 5):
+        x = torch.randn(B, C, T, device=dev) * 0.5
+        cond = torch.randn(B, C, device=dev) * 0.3
+        for k in (3, 7, 11):
+            w1 = torch.randn(C, C, k, device=dev) / (C * k) ** 0.5
+            w2 = torch.randn(C, C // 2, k, device=dev) / (C * k / 2) ** 0.5
+            e1 = ops.pack_conv(w1, torch.zeros(C, device=dev), dilation=d, gate=True)
+            e2 = ops.pack_conv(w2, torch.zeros(C, device=dev))
+            s1 = ops.to_lowp(e1, ops.WDT_F32S, min_rows=0)
+            s2 = ops.to_lowp(e2, ops.WDT_F32S, min_rows=0)
+            y = torch.empty(B, C, T, device=dev)
+            if ops.resblock_pair_supported(e1, e2, T):
+                pe = ops.resblock_pair_desc(e1, e2, x, y, cond=cond)
+                te = timeit(lambda: ops.resblock_pair_launch(pe, B, dev))
+            else:
+                gb = torch.empty(B, C // 2, T, device=dev)
+                ds = [make_desc(e1, x, make_out(gb), in_slope=0.1, cond=cond),
+                      make_desc(e2, gb, make_out(y, res=x))]
+                te = timeit(lambda: ops.conv1d_launch_seq(ds, B, dev))
+            ps = ops.resblock_pair_desc(s1, s2, x, y, cond=cond)
+            ts = timeit(lambda: ops.resblock_pair_launch(ps, B, dev, ops.WDT_F32P))
+            f1 = ops.resblock_pair_flops(ps, B)
+            tex += te
+            tsp += ts
+            print(f"C32.k{k}d{d}  exact (shipped) {te*1e3:7.1f} us {f1/te/1e9:6.1f} TF/s"
+                  f"   split fused {ts*1e3:7.1f} us {f1/ts/1e9:6.1f} TF/s", flush=True)
+    print(f"TOTAL C32 exact {tex:.3f} ms  split fused {tsp:.3f} ms")

@@ -1,5 +1,5 @@
 // resblock_f32p.hip — one ResBlock2 dilation pair of the fp32 Generator's
-// 64-, 128- and 256-channel stages as ONE kernel, in the split-fp32
+// 32-, 64-, 128- and 256-channel stages as ONE kernel, in the split-fp32
 // arithmetic of the pre-split-weight conv (VITS_WDT_F32P, conv1d_impl.h):
 //
 //   y = x + c2( tanh(a + sa) * sigmoid(b + sb) ) ,   (a | b) = c1(lrelu(x, 0.1))
@@ -32,7 +32,7 @@
 // the same k-step order (slab-major, then tap), the same six products per
 // fragment pair in the same order, the same gate and epilogue expressions
 // (tests/test_resblock_f32p_gpu.py checks equality).  Tiles: C = 64 ->
-// 64 x 256 (1 x 4 waves), C = 128 -> 128 x 128 (2 x 2), two workgroups per
+// 64 x 256 (1 x 4 waves; C = 32: 32 x 256), C = 128 -> 128 x 128 (2 x 2), two workgroups per
 // CU; C = 256 -> 256 x 128 (4 x 2 waves, one 512-thread workgroup per CU:
 // the same two waves per SIMD).  Every launch holds up to 3 independent
 // pairs (the branches of a stage).
@@ -56,7 +56,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-__host__ __device__ constexpr int rp_ng(int C) { return C == 64 ? 256 : 128; }
+__host__ __device__ constexpr int rp_ng(int C) { return C <= 64 ? 256 : 128; }
 // threads: 4 waves (C = 64, 128), 8 waves of 64 x 64 (C = 256: 256 x 128)
 __host__ __device__ constexpr int rp_threads(int C) { return C == 256 ? 512 : 256; }
 // c1 channels per staged X chunk (one barrier each): 16 where two workgroups
@@ -81,11 +81,11 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
     const RpGroup G) {
   constexpr int H = C / 2;
   constexpr int NT = rp_threads(C);
-  constexpr int WAVES_M = C / 64;
+  constexpr int WAVES_M = C >= 64 ? C / 64 : 1;
   constexpr int WAVES_N = NT / 64 / WAVES_M;
   constexpr int NG = 64 * WAVES_N;
   static_assert(NG == rp_ng(C), "tile columns");
-  constexpr int TM = 2, TN = 2;  // 64 x 64 per wave
+  constexpr int TM = C >= 64 ? 2 : 1, TN = 2;  // 64 x 64 per wave (C = 32: 32 x 64)
   constexpr int KC = rp_kc(C);          // c1 channels per staged chunk
   constexpr int KCP = KC + 4;           // X chunk row pitch (bf16)
   constexpr int GP = H + 8;              // G row pitch (bf16): 16-byte rows
@@ -441,7 +441,8 @@ int rp_check(const vits_resblock_pair_desc& d) {
   VITS_CHECK_ARG(d.x && d.w1 && d.w2 && d.y);
   // other workgroups still read x (halos, residual): never write in place
   VITS_CHECK_ARG(reinterpret_cast<const void*>(d.y) != reinterpret_cast<const void*>(d.x));
-  VITS_CHECK_SHAPE(d.channels == 64 || d.channels == 128 || d.channels == 256);
+  VITS_CHECK_SHAPE(d.channels == 32 || d.channels == 64 || d.channels == 128 ||
+                   d.channels == 256);
   VITS_CHECK_SHAPE(d.k >= 1 && d.k <= 15 && (d.k & 1) == 1 && d.dil >= 1 && d.t_len > 0);
   VITS_CHECK_SHAPE((d.k - 1) * d.dil <= 96);  // window within the staging units
   // images [cin_pad/16][k][2][3][m_pad][8] bf16, rows = C (c1 gate-interleaved / c2)
@@ -475,7 +476,9 @@ extern "C" int vits_resblock_pair_f32p_forward(const vits_resblock_pair_desc* d,
   }
   hipStream_t s = as_stream(stream);
   int rc;
-  if (d[0].channels == 64)
+  if (d[0].channels == 32)
+    rc = rp_launch<32>(g, s);
+  else if (d[0].channels == 64)
     rc = rp_launch<64>(g, s);
   else if (d[0].channels == 128)
     rc = rp_launch<128>(g, s);

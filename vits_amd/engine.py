@@ -168,10 +168,17 @@ class GeneratorPlan:
                     w1, b1 = _conv_eff(c1)
                     w2, b2 = _conv_eff(c2)
                     wc, bc = _linear_eff(cs)
-                    pairs.append((pack_conv(w1, b1, dilation=c1.dilation[0], padding=c1.padding[0],
-                                            gate=True),
-                                  pack_conv(w2, b2, dilation=c2.dilation[0], padding=c2.padding[0]),
-                                  conds.add(wc, bc)))
+                    p1 = pack_conv(w1, b1, dilation=c1.dilation[0], padding=c1.padding[0],
+                                   gate=True)
+                    p2 = pack_conv(w2, b2, dilation=c2.dilation[0], padding=c2.padding[0])
+                    alt = None
+                    if (ops.PACK_PRECISION.wdtype == ops.WDT_F32S and p1.wdtype == ops.WDT_F32
+                            and p2.wdtype == ops.WDT_F32):
+                        # a split-fp32 model's 32-row convs stay exact fp32 as
+                        # single convs; the fused split pair takes them too
+                        alt = (ops.to_lowp(p1, ops.WDT_F32S, min_rows=0),
+                               ops.to_lowp(p2, ops.WDT_F32S, min_rows=0))
+                    pairs.append((p1, p2, conds.add(wc, bc), alt))
                 blocks.append(pairs)
             self.stages.append(blocks)
         self.cond_w, self.cond_b = conds.finish()
@@ -234,24 +241,37 @@ class GeneratorPlan:
         C, T = xu.shape[1], xu.shape[2]
         io16 = 2 if xu.dtype != torch.float32 else 0  # (2: inference decoder, conv1d.hip ga16)
 
-        def can_fuse(pr):
+        def fused_layers(pr):
+            """(c1, c2) the fused pair kernel runs for this pair, or None."""
             if io16:  # 16-bit model, 16-bit activations: csrc/resblock16.hip
-                return ops.resblock_pair16_supported(pr[0], pr[1], xu)
-            return _FUSED_PAIRS and (ops.resblock_pair_supported(pr[0], pr[1], T) or
-                                     ops.resblock_pair_f32p_supported(pr[0], pr[1], xu))
+                return pr[:2] if ops.resblock_pair16_supported(pr[0], pr[1], xu) else None
+            if not _FUSED_PAIRS:
+                return None
+            # split fp32 (resblock_f32p.hip) first: on the 32-channel stage it
+            # beats the exact pair (k=7 -30 %, k=11 -35 %, tools/rbp_bench.py)
+            for c1, c2 in ((pr[0], pr[1]),) + ((pr[3],) if pr[3] is not None else ()):
+                if ops.resblock_pair_f32p_supported(c1, c2, xu):
+                    return c1, c2
+            return pr[:2] if ops.resblock_pair_supported(pr[0], pr[1], T) else None
 
-        fused = [[can_fuse(pr) for pr in pairs] for pairs in blocks]
+        fused = [[fused_layers(pr) for pr in pairs] for pairs in blocks]
 
         def pair_desc(j, p, dst, **kw):
             fn = ops.resblock_pair16_desc if io16 else ops.resblock_pair_desc
-            return fn(blocks[j][p][0], blocks[j][p][1], cur[j], dst, cond=cond,
-                      cond_offset=blocks[j][p][2], lengths=lengths, **kw)
+            c1, c2 = fused[j][p]
+            return fn(c1, c2, cur[j], dst, cond=cond, cond_offset=blocks[j][p][2],
+                      lengths=lengths, **kw)
 
-        def pair_launch(descs):
+        def pair_launch(js, p, dsts, **kw):
+            """The fused pairs of branches js (one launch per weight type)."""
             if io16:
-                ops.resblock_pair16_launch(descs, B, dev, blocks[0][0][0].wdtype)
-            else:
-                ops.resblock_pair_launch(descs, B, dev, blocks[0][0][0].wdtype)
+                ops.resblock_pair16_launch(tuple(pair_desc(j, p, d, **kw) for j, d in zip(js, dsts)),
+                                           B, dev, blocks[0][0][0].wdtype)
+                return
+            for wdt in sorted({fused[j][p][0].wdtype for j in js}):
+                sel = [(j, d) for j, d in zip(js, dsts) if fused[j][p][0].wdtype == wdt]
+                ops.resblock_pair_launch(tuple(pair_desc(j, p, d, **kw) for j, d in sel), B, dev,
+                                         wdt)
         tmp = [[torch.empty_like(xs), torch.empty_like(xs)] for _ in range(nk)]
         gbuf = [None if all(fused[j]) else
                 torch.empty(B, C // 2, T, device=dev, dtype=xu.dtype) for j in range(nk)]
@@ -270,7 +290,7 @@ class GeneratorPlan:
             if p < npairs - 1:
                 dst = [tmp[j][p & 1] for j in range(nk)]
                 if fj:
-                    pair_launch(tuple(pair_desc(j, p, dst[j]) for j in fj))
+                    pair_launch(fj, p, [dst[j] for j in fj])
                 if cj:
                     descs = grouped(c1_desc(j, p) for j in cj)
                     descs += grouped(make_desc(blocks[j][p][1], gbuf[j],
@@ -291,7 +311,7 @@ class GeneratorPlan:
             for j in range(nk):
                 kw = dict(accumulate=j > 0, post_div=float(nk) if j == nk - 1 else 1.0)
                 if fused[j][p]:
-                    pair_launch(pair_desc(j, p, xs, **kw))
+                    pair_launch([j], p, [xs], **kw)
                 else:
                     ops.conv1d_launch_seq([make_desc(blocks[j][p][1], gbuf[j],
                                                      make_out(xs, res=cur[j], **kw),

@@ -290,7 +290,7 @@ def _f32s_min_rows() -> int:
     return F32S_MIN_ROWS or (64 if SPLIT_W else 128)
 
 
-def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
+def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16, min_rows: Optional[int] = None) -> PackedConv:
     """Re-pack an fp32 layer for the 16-bit-MFMA kernel variant (bf16 or
     fp16 operands, fp32 accumulation): K-chunks of 16 channels, W as
     [cin_pad/16][k][2][m_pad][8] (one 16-byte A fragment per row and 8
@@ -299,7 +299,8 @@ def to_lowp(layer: PackedConv, wdtype: int = WDT_BF16) -> PackedConv:
     if layer.wdtype != WDT_F32 or wdtype == WDT_F32:
         return layer
     if wdtype == WDT_F32S:
-        if layer.m < _f32s_min_rows():
+        # (min_rows: the fused split-fp32 pairs take the 32-row convs too)
+        if layer.m < (_f32s_min_rows() if min_rows is None else min_rows):
             return layer
         kc = 16
         w32 = layer.w[:layer.cin]
@@ -640,8 +641,11 @@ def resblock_pair_supported(c1: PackedConv, c2: PackedConv, T: int) -> bool:
 # k=11 -2 %; C=128 k=3 -25 %, k=7 -4..-8 %, k=11 +-0 (the c1 phase
 # recomputes c2's halo: 10 of 128 columns at k=11); C=256 (one 512-thread
 # workgroup per CU, 543 tiles per utterance batch: 2.1 rounds of the chip)
-# k=3 -17 %, k=7 / k=11 +30..40 %
-F32P_PAIR_MAX_K = {64: 11, 128: 7, 256: 3}
+# k=3 -17 %, k=7 / k=11 +30..40 %.  The 32-channel stage's convs stay exact
+# fp32 as single convs (32 rows), but its pairs run split fused too
+# (engine.GeneratorPlan keeps split images beside them): vs the shipped exact
+# pair / two-conv path k=3 -2..-5 %, k=7 -25..-33 %, k=11 -34..-35 %
+F32P_PAIR_MAX_K = {32: 11, 64: 11, 128: 7, 256: 3}
 
 
 def resblock_pair_f32p_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -> bool:
