@@ -742,7 +742,7 @@ def main():
             traffic, tsrc = pmc_traffic()
             kernel_table = conv_kernel_table(timer, args.steps)
             roof = {"bound": "mfma",
-                    "kernel": "conv1d_mfma_kernel + resblock_pair_kernel (every conv / fused "
+                    "kernel": "conv1d_mfma_kernel + resblock_f32p_kernel (every conv / fused "
                               "ResBlock2-pair launch of a step)",
                     "achieved": round(achieved, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4),

@@ -227,11 +227,16 @@ def test_expand_prior(device):
     _close(out, ref, tol=1e-6, what="expand")
 
 
-def test_conv_post_tanh(device):
+@pytest.mark.parametrize("T,dt", [(1234, torch.float32), (1236, torch.float32),
+                                  (9216, torch.float32), (9216, torch.bfloat16),
+                                  (4000, torch.float16), (1230, torch.bfloat16)])
+def test_conv_post_tanh(device, T, dt):
+    """The Generator tail: element-wise staging (T % 4 != 0) and the 4-step
+    block form (T % 4 == 0), fp32 and 16-bit last-stage activations."""
     g = torch.Generator().manual_seed(11)
-    x = torch.randn(2, 32, 1234, generator=g)
+    x = (torch.randn(2, 32, T, generator=g)).to(dt)
     w = torch.randn(1, 32, 7, generator=g) * 0.2
-    ref = torch.tanh(F.conv1d(F.leaky_relu(x), w, None, padding=3))
+    ref = torch.tanh(F.conv1d(F.leaky_relu(x.float()), w, None, padding=3))
     out = ops.conv_post_tanh(x.to(device), w.to(device))
     _close(out, ref, what="conv_post")
 

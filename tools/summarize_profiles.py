@@ -31,7 +31,8 @@ for r in stats:
     name = r["Name"]
     short = name.replace("(anonymous namespace)::", "").replace("void ", "")
     key = ("conv1d_mfma_kernel" if "conv1d_mfma_kernel" in name else
-           "resblock_pair_kernel" if ("resblock_pair_kernel" in name or "resblock16_kernel" in name) else
+           "resblock_pair_kernel" if any(k in name for k in ("resblock_pair_kernel", "resblock16_kernel",
+                                                    "resblock_f32p_kernel")) else
            short.split("(")[0].split("<")[0][:60])
     fam[key][0] += int(r["Calls"])
     fam[key][1] += float(r["TotalDurationNs"])
@@ -45,7 +46,8 @@ def pmc(name):
     # the bench's dominant kernel: every conv launch of the step (the conv
     # kernel and the fused ResBlock2 pair kernel)
     vals = [float(r["Counter_Value"]) for r in rows
-            if any(k in r["Kernel_Name"] for k in ("conv1d_mfma_kernel", "resblock_pair_kernel", "resblock16_kernel"))]
+            if any(k in r["Kernel_Name"] for k in ("conv1d_mfma_kernel", "resblock_pair_kernel",
+                                               "resblock16_kernel", "resblock_f32p_kernel"))]
     return vals
 
 
@@ -58,7 +60,7 @@ summary = {
     "tag": tag,
     "kernel_families": families,
     "conv_kernels": {
-        "kernels": "conv1d_mfma_kernel + resblock_pair_kernel",
+        "kernels": "conv1d_mfma_kernel + resblock_pair_kernel + resblock_f32p_kernel",
         "pmc_launches": n,
         "hbm_fetch_bytes_per_launch": round(fetch_b),
         "hbm_write_bytes_per_launch": round(write_b),

@@ -341,6 +341,67 @@ __global__ __launch_bounds__(256) void conv_post_tanh_kernel(const XT* __restric
   y[(int64_t)b * t_len + t] = tanhf(acc);
 }
 
+// Aligned form (T % 4 == 0, 4-element-aligned rows, ksize <= 9): every
+// thread issues all its 4-step block loads of the CPC-channel window at once
+// (16 bytes fp32 / 8 bytes 16-bit per load) before the first is used - the
+// grouped form above waits ~channels / 8 load round trips per workgroup (122
+// us for the B=16 decoder tail, ~1.6 TB/s).  Window columns [t0 - 4, t0 +
+// CP_T + 4): tap j of output t reads column t - t0 + 1 + j.
+template <typename XT, int CPC>
+__global__ __launch_bounds__(256) void conv_post_tanh_v4_kernel(const XT* __restrict__ x,
+                                                                int64_t x_bstride, int x_cstride,
+                                                                const float* __restrict__ w,
+                                                                float* __restrict__ y, int t_len,
+                                                                int ksize) {
+  constexpr int W = CP_T + 8;         // window columns
+  constexpr int NB = W / 4;           // 4-step blocks per channel row
+  constexpr int NU = (CPC * NB + 255) / 256;
+  typedef XT x4 __attribute__((ext_vector_type(4)));
+  __shared__ float xs[CPC * W];
+  __shared__ float wsm[CPC * 9];
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * CP_T;
+  const XT* xb = x + (int64_t)b * x_bstride;
+  for (int i = threadIdx.x; i < CPC * ksize; i += 256) wsm[i] = w[i];
+  x4 v[NU];
+  bool ok[NU];
+#pragma unroll
+  for (int q = 0; q < NU; ++q) {
+    const int u = threadIdx.x + 256 * q;
+    const int c = u / NB;
+    const int tt = t0 - 4 + 4 * (u - c * NB);
+    ok[q] = u < CPC * NB && tt >= 0 && tt < t_len;  // a block is all in or all out
+    v[q] = *reinterpret_cast<const x4*>(ok[q] ? xb + (int64_t)c * x_cstride + tt : xb);
+  }
+#pragma unroll
+  for (int q = 0; q < NU; ++q) {
+    const int u = threadIdx.x + 256 * q;
+    if (u < CPC * NB) {
+      const int c = u / NB;
+      float4 f;
+      float* fe = reinterpret_cast<float*>(&f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = ok[q] ? (float)v[q][e] : 0.f;
+        fe[e] = a < 0.f ? 0.01f * a : a;
+      }
+      *reinterpret_cast<float4*>(xs + c * W + 4 * (u - c * NB)) = f;
+    }
+  }
+  __syncthreads();
+  const int tl = threadIdx.x;
+  const int t = t0 + tl;
+  if (t >= t_len) return;
+  const int off = 4 - (ksize - 1) / 2;  // window column of tap 0
+  float acc = 0.f;
+  for (int c = 0; c < CPC; ++c) {
+    const float* xr = xs + c * W + tl + off;
+    const float* wr = wsm + c * ksize;
+    for (int j = 0; j < ksize; ++j) acc += wr[j] * xr[j];
+  }
+  y[(int64_t)b * t_len + t] = tanhf(acc);
+}
+
 }  // namespace
 
 extern "C" int vits_linear_forward(const float* g, int64_t g_bstride, const float* w,
@@ -409,6 +470,22 @@ extern "C" int vits_conv_post_tanh_lowp(const void* x, int64_t x_bstride, int32_
   VITS_CHECK_SHAPE(lds <= 64 * 1024);
   dim3 grid((t_len + CP_T - 1) / CP_T, batch);
   hipStream_t s = as_stream(stream);
+  const int esz = xdtype == VITS_WDT_F32 ? 4 : 2;
+  if (channels == 32 && ksize <= 9 && (t_len & 3) == 0 && (x_cstride & 3) == 0 &&
+      (x_bstride & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & (4 * esz - 1)) == 0) {
+    // the decoder tail (upsample_initial_channel / 2^4 = 32 channels, k = 7)
+    if (xdtype == VITS_WDT_BF16)
+      hipLaunchKernelGGL((conv_post_tanh_v4_kernel<__bf16, 32>), grid, dim3(256), 0, s,
+                         static_cast<const __bf16*>(x), x_bstride, x_cstride, w, y, t_len, ksize);
+    else if (xdtype == VITS_WDT_F16)
+      hipLaunchKernelGGL((conv_post_tanh_v4_kernel<_Float16, 32>), grid, dim3(256), 0, s,
+                         static_cast<const _Float16*>(x), x_bstride, x_cstride, w, y, t_len,
+                         ksize);
+    else
+      hipLaunchKernelGGL((conv_post_tanh_v4_kernel<float, 32>), grid, dim3(256), 0, s,
+                         static_cast<const float*>(x), x_bstride, x_cstride, w, y, t_len, ksize);
+    return vits_launch_status();
+  }
   if (xdtype == VITS_WDT_BF16)
     hipLaunchKernelGGL(conv_post_tanh_kernel<__bf16>, grid, dim3(256), lds, s,
                        static_cast<const __bf16*>(x), x_bstride, x_cstride, w, y, channels, t_len,
