@@ -341,6 +341,9 @@ def kernels_leg(device):
                 "cpu_baseline": mas_cpu,
                 "vs_cpu": round(mas_cpu["ms"] / mas_ms, 1)},
         "neg_cent": {"ms": round(nc_ms, 4), "TFLOPs": round(nc_flops / nc_ms / 1e9, 2),
+                     "arith": "split-f32 (three exact bf16 terms, six bf16 MFMAs per product)",
+                     "frac": round(nc_flops / nc_ms / 1e9 / (FP16_MFMA_PEAK_TFLOPS / 6), 4),
+                     "peak": round(FP16_MFMA_PEAK_TFLOPS / 6, 1),
                      "frac_fp32_mfma": round(nc_flops / nc_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4),
                      "shape": f"B={B} C={C} t_t={Tt} t_s={Ts}"},
         "mrstft_mag_fwd": {"ms": round(fwd_ms, 4), "GBps": round(fwd_bytes / fwd_ms / 1e6, 1),
