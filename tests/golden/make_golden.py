@@ -39,6 +39,9 @@ Fixtures (npz, float32 unless noted):
                       gradient statistics and post-step parameter statistics
                       (RAdam for D, AdamW for G as the reference builds them);
                       train_step_config.json the config.
+  base_c5.npz         one C5 long-form utterance (Tx=500, Ty=2500) through
+                      the reference's bf16 model and its fp32 model:
+                      waveform windows / statistics, reference SNR
   base_c1.npz         the C1 headline utterance (configs/base.json, Tx=100,
                       Ty=500, models.py:568-575): infer_p1 / infer_p2 outputs,
                       waveform head / middle windows, per-block rms of the
@@ -511,6 +514,58 @@ def make_c1(models, m=None):
     np.savez_compressed(os.path.join(HERE, "base_c1.npz"), **arrs)
 
 
+def c5_inputs():
+    """One BASELINE C5 utterance (Tx=500, 5 frames per token -> Ty=2500,
+    480,000 samples): bench.make_inputs(1, 500, 2500, seed=4321)."""
+    g = torch.Generator().manual_seed(4321)
+    Tx, Ty = 500, 2500
+    dur = torch.full((1, 1, Tx), float(Ty // Tx))
+    m_p = torch.randn(1, 192, Tx, generator=g)
+    s_p = torch.rand(1, 192, Tx, generator=g) + 0.3
+    gg = torch.randn(1, 1024, generator=g) * 0.5
+    noise = torch.randn(1, 192, Ty, generator=g) * 0.707
+    return dur, m_p, s_p, gg, noise
+
+
+def make_c5(models):
+    """The C5 long-form utterance through the reference's own bf16 model
+    (models.py:568-575 after model.to(torch.bfloat16), torch-CPU bf16
+    convolutions) and its fp32 model: windows, statistics and per-block rms
+    of both waveforms, plus the reference's bf16-vs-fp32 SNR - the yardstick
+    the HIP bf16 path is held to (tests/test_configs_gpu.py)."""
+    import commons
+
+    cfg = base_cfg()
+    m = models.SynthesizerTrn(cfg["data"]["text_channels"],
+                              cfg["data"]["filter_length"] // 2 + 1,
+                              cfg["train"]["segment_size"] // cfg["data"]["hop_length"],
+                              n_speakers=cfg["data"]["n_speakers"], **cfg["model"]).eval()
+    deterministic_fill_(m)
+    dur, m_p, s_p, gg, noise = c5_inputs()
+    attn = commons.infer_path(dur, 500, 2500)
+    with torch.no_grad():
+        w32 = m.infer_p2(attn, m_p, s_p, gg, noise).float()
+        m16 = m.to(torch.bfloat16)
+        w16 = m16.infer_p2(*(t.to(torch.bfloat16) for t in (attn, m_p, s_p, gg, noise))).float()
+
+    def snr(a, b):
+        a, b = a.double().flatten(), b.double().flatten()
+        return float(10 * torch.log10((b * b).sum() / ((a - b) ** 2).sum()))
+
+    arrs = dict(in_sums=np.array([m_p.double().sum(), s_p.double().sum(), gg.double().sum(),
+                                  noise.double().sum()]),
+                ref_snr_bf16_vs_fp32=np.float64(snr(w16, w32)))
+    for tag, w in (("w16", w16), ("w32", w32)):
+        wd = w.double().flatten()
+        arrs[tag + "_stats"] = np.array([wd.sum(), wd.abs().sum(), (wd * wd).sum(),
+                                         wd.abs().max()])
+        arrs[tag + "_block_rms"] = np32(w[0, 0].view(-1, 1920).pow(2).mean(1).sqrt())
+        for name, start in (("head", 0), ("mid", 240000), ("tail", 480000 - 16384)):
+            arrs[f"{tag}_{name}"] = np32(w[0, 0, start:start + 16384])
+    np.savez_compressed(os.path.join(HERE, "base_c5.npz"), **arrs)
+    print("C5 reference bf16 vs fp32 SNR %.2f dB" % arrs["ref_snr_bf16_vs_fp32"])
+
+
 def main():
     torch.set_num_threads(8)
     models, stft_loss = _ref()
@@ -518,10 +573,11 @@ def main():
         for name in sys.argv[1:]:
             {"mpd": lambda: make_mpd(models), "mwsd": lambda: make_mwsd(stft_loss),
              "train_step": lambda: make_train_step(models, stft_loss),
-             "c1": lambda: make_c1(models)}[name]()
+             "c1": lambda: make_c1(models), "c5": lambda: make_c5(models)}[name]()
         return
     m = make_base(models)
     make_c1(models, m)
+    make_c5(models)
     make_tiny(models)
     make_mrstft(stft_loss)
     make_mpd(models)

@@ -74,6 +74,51 @@ def test_c1_single_call_infer_vs_reference(base, device):
     assert rel_err(o, gd["infer_o"]) < 1e-4
 
 
+def test_c5_longform_bf16_vs_reference_bf16_model(base, device):
+    """One C5 utterance (Tx=500, Ty=2500, 480,000 samples) against the
+    REFERENCE's own bf16 model (models.py after model.to(torch.bfloat16),
+    recorded on CPU: tests/golden/base_c5.npz) and its fp32 model.
+    * fp32 HIP vs reference fp32: SNR >= 60 dB, as C1.
+    * bf16 HIP vs reference fp32: no worse than the reference's own bf16
+      model is (its SNR vs fp32, 37.6 dB, minus 3 dB).
+    * bf16 HIP vs reference bf16: two independent bf16 roundings of the
+      same network, each ~38 dB from fp32; their noise powers add, so the
+      bar is the reference's SNR minus 6 dB.
+    Windows: head / middle / tail, 16,384 samples each."""
+    from bench import make_inputs
+
+    gd = golden("base_c5.npz")
+    inputs = make_inputs(1, 500, 2500, device, seed=4321)
+    sums = np.array([inputs[i].double().sum().item() for i in (1, 2, 3, 4)])
+    assert np.allclose(sums, gd["in_sums"], rtol=0, atol=1e-6 * np.abs(gd["in_sums"]).max()), \
+        "input regeneration drifted"
+    with torch.no_grad():
+        w32 = base.infer_p2(*inputs).float().cpu()
+        m16 = base_model(device).to(torch.bfloat16)
+        run = m16.capture_infer_p2(1, 500, 2500)
+        w16 = run(*inputs).float().cpu()
+    torch.cuda.synchronize()
+    ref_snr = float(gd["ref_snr_bf16_vs_fp32"])
+
+    def cat(w):
+        return torch.cat([w[0, 0, s:s + 16384] for s in (0, 240000, 480000 - 16384)])
+
+    def cat_ref(tag):
+        return torch.from_numpy(np.concatenate([gd[f"{tag}_{n}"] for n in ("head", "mid", "tail")]))
+
+    s32 = snr_db(cat(w32), cat_ref("w32"))
+    s16_32 = snr_db(cat(w16), cat_ref("w32"))
+    s16_16 = snr_db(cat(w16), cat_ref("w16"))
+    print(f"C5: fp32 vs ref fp32 {s32:.1f} dB; bf16 vs ref fp32 {s16_32:.1f} dB "
+          f"(reference bf16: {ref_snr:.1f} dB); bf16 vs ref bf16 {s16_16:.1f} dB")
+    assert s32 >= 60.0
+    assert s16_32 >= ref_snr - 3.0
+    assert s16_16 >= ref_snr - 6.0
+    # loudness envelope (per 1920-sample block rms) of the bf16 waveform
+    rms = w16[0, 0].view(-1, 1920).pow(2).mean(1).sqrt().numpy()
+    assert np.abs(rms - gd["w16_block_rms"]).max() <= 0.05 * gd["w16_block_rms"].max()
+
+
 def test_c5_longform_bf16_graph_vs_fp32(base, device):
     """BASELINE C5 shape: B=4, Tx=500, Ty=2500 (480,000 samples each), bf16
     model replayed from one hipGraph, vs the fp32 HIP output."""
