@@ -1,8 +1,7 @@
 """A/B of bench.py's train (C4, B=32, captured) and long-form (C5, bf16,
 captured) legs under python-side settings, one arm per process:
-  python tools/ab_legs.py [--xb16 N] [--legs train,longform]
---xb16: the 16-bit X staging budget of 128-column tiles (ops.XB16_BUDGET;
-6144 = the round-4 kc choice).  VITS_AMD_LIB picks the library build.
+  python tools/ab_legs.py [--legs train,longform]
+VITS_AMD_LIB picks the library build (tools/ab_build.sh).
 Prints one JSON line."""
 import argparse
 import json
@@ -14,16 +13,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from vits_amd import ops  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--xb16", type=int, default=None)
 ap.add_argument("--legs", default="train,longform")
 a = ap.parse_args()
-if a.xb16:
-    ops.XB16_BUDGET[128] = a.xb16
 dev = torch.device("cuda:0")
-out = {"lib": os.environ.get("VITS_AMD_LIB", "default"), "xb16": ops.XB16_BUDGET[128]}
+out = {"lib": os.environ.get("VITS_AMD_LIB", "default")}
 legs = a.legs.split(",")
 if "train" in legs:
     args = types.SimpleNamespace(train_eager=False, train_batch=32, tx=100, ty=500,
