@@ -41,6 +41,10 @@ class MultiHeadAttention(nn.Module):
         nn.init.xavier_uniform_(self.conv_q.weight)
         nn.init.xavier_uniform_(self.conv_k.weight)
         nn.init.xavier_uniform_(self.conv_v.weight)
+        # (served by train_ops.conv1d_cat in self-attention, which packs the
+        # concatenated weight: train_ops.prepacked skips them)
+        for m in (self.conv_q, self.conv_k, self.conv_v):
+            m._vits_cat = True
 
     def forward(self, x, c, attn_mask=None, lengths=None):
         """lengths (int [B], optional): the key / query lengths attn_mask was

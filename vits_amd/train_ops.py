@@ -40,6 +40,7 @@ from __future__ import annotations
 import collections
 import contextlib
 import os
+import sys
 
 import torch
 import torch.nn.functional as F
@@ -190,7 +191,10 @@ def prepacked(net: nn.Module):
     wdt = autocast_wdtype("cuda") if HIP_TRAIN else None
     mods = []
     if PREPACK and wdt is not None and _io16(wdt):
+        # (q / k / v projections come concatenated from conv1d_cat: QKV_CAT)
+        skip_cat = getattr(sys.modules.get(__package__ + ".attentions"), "QKV_CAT", False)
         mods = [m for m in net.modules() if supported(m)
+                and not (skip_cat and getattr(m, "_vits_cat", False))
                 and any(p.is_cuda for p in m.parameters(recurse=False))]
     gates = [bool(GATE_FUSED and getattr(m, "_vits_gate", False)) for m in mods]
     if not mods:
