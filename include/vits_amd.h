@@ -504,8 +504,10 @@ int vits_resblock_pair_kc(int channels, int k, int dil, int* kc1, int* kc2);
 /* x and y are [B][C][T] tensors of that type (the float pointers of the  */
 /* descriptor reinterpreted), w1 / w2 the 16-bit images                   */
 /* [cin_pad/16][k][2][m_pad][8] of vits_conv1d_desc (w1's rows gate-      */
-/* interleaved); kc1 / kc2 are ignored.  C = 32, 64 or 128, odd k,      */
-/* (k - 1) * dil <= 96, T % 4 == 0.                                       */
+/* interleaved); kc1 / kc2 are ignored.  C = 32, 64, 128 or 256 (the    */
+/* 256-channel pairs run csrc/resblock_f32p.hip's streamed-K tile in its  */
+/* 16-bit mode; not for the _mean variant), odd k, (k - 1) * dil <= 96,  */
+/* T % 4 == 0.                                                            */
 int vits_resblock_pair16_forward(const vits_resblock_pair_desc* d, int n, int batch, int wdtype,
                                  void* stream);
 /* The last pairs of a stage's n branches as ONE launch: d[0].y receives  */

@@ -538,6 +538,7 @@ def test_resblock_pair_fused(device, C, k, dil, T):
 @pytest.mark.parametrize("C,k,dil,T", [
     (32, 3, 1, 12), (32, 11, 5, 300), (64, 7, 3, 2052), (64, 3, 5, 48), (32, 7, 1, 9216),
     (64, 11, 5, 1000), (64, 11, 1, 500), (128, 3, 1, 500), (128, 11, 5, 1000), (128, 7, 3, 124),
+    (256, 3, 1, 132), (256, 11, 5, 1000), (256, 7, 3, 300),
 ])
 @pytest.mark.parametrize("wdt", [ops.WDT_BF16, ops.WDT_F16])
 def test_resblock_pair16_fused(device, C, k, dil, T, wdt):
@@ -546,8 +547,9 @@ def test_resblock_pair16_fused(device, C, k, dil, T, wdt):
     LDS as the two-conv path rounds it in HBM) against the pair in fp64 on
     the same 16-bit-rounded inputs and weights: tiles shorter than the
     sequence, ends inside a tile, the three-branch grouped launch and the
-    branch-mean epilogue.  Tolerance: 2 roundings of the operand type
-    (bf16 2e-2, fp16 3e-3 of the output magnitude)."""
+    branch-mean epilogue.  256 channels: csrc/resblock_f32p.hip's 16-bit
+    mode (no one-launch branch mean there).  Tolerance: 2 roundings of the
+    operand type (bf16 2e-2, fp16 3e-3 of the output magnitude)."""
     dt = {ops.WDT_BF16: torch.bfloat16, ops.WDT_F16: torch.float16}[wdt]
     tol = 2e-2 if wdt == ops.WDT_BF16 else 3e-3
     g = torch.Generator().manual_seed(C + k + dil + T + wdt)
@@ -582,6 +584,8 @@ def test_resblock_pair16_fused(device, C, k, dil, T, wdt):
             B, device, wdt)
     torch.cuda.synchronize()
     _close(acc, (refs[0] + refs[1] + refs[2]) / 3, tol=2 * tol, what="mean")
+    if C == 256:
+        return
     # the branch mean as ONE launch (vits_resblock_pair16_mean_forward)
     mean = torch.full((B, C, T), float("nan"), device=device, dtype=dt)
     ops.resblock_pair16_launch(tuple(

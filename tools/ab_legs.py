@@ -16,9 +16,14 @@ import bench  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--legs", default="train,longform")
+ap.add_argument("--pair16-256", type=int, default=None,
+                help="ops.PAIR16_256_MAX_K (0: the 256-channel stage's two-conv path)")
 a = ap.parse_args()
+if a.pair16_256 is not None:
+    from vits_amd import ops
+    ops.PAIR16_256_MAX_K = a.pair16_256
 dev = torch.device("cuda:0")
-out = {"lib": os.environ.get("VITS_AMD_LIB", "default")}
+out = {"lib": os.environ.get("VITS_AMD_LIB", "default"), "pair16_256": a.pair16_256}
 legs = a.legs.split(",")
 if "train" in legs:
     args = types.SimpleNamespace(train_eager=False, train_batch=32, tx=100, ty=500,

@@ -408,10 +408,16 @@ int r16_check(const vits_resblock_pair_desc& d) {
 
 }  // namespace
 
+// resblock_f32p.hip: the 256-channel pairs (a streamed-K tile)
+int vits_rp16_256(const vits_resblock_pair_desc* d, int n, int batch, int wdtype,
+                  hipStream_t s);
+
 static int r16_run(const vits_resblock_pair_desc* d, int n, int batch, int wdtype, int mean,
                    void* stream) {
   if (!d || n < 1 || n > R16_GROUP || batch < 1) return VITS_E_ARG;
   if (wdtype != VITS_WDT_BF16 && wdtype != VITS_WDT_F16) return VITS_E_ARG;
+  // a 256-channel window does not fit this kernel's whole-window staging
+  if (d[0].channels == 256 && !mean) return vits_rp16_256(d, n, batch, wdtype, as_stream(stream));
   R16Group g;
   g.n = n;
   g.batch = batch;

@@ -36,6 +36,14 @@
 // CU; C = 256 -> 256 x 128 (4 x 2 waves, one 512-thread workgroup per CU:
 // the same two waves per SIMD).  Every launch holds up to 3 independent
 // pairs (the branches of a stage).
+//
+// MODE 1 / 2: the same tile for a bf16 / fp16 model's 256-channel pairs
+// (vits_resblock_pair16_forward routes them here - resblock16.hip stages a
+// whole window, which 256 channels do not fit): 16-bit x / y in HBM, one
+// operand plane, one MFMA per fragment pair, the gated tensor rounded to the
+// 16-bit type in LDS as the two-conv path rounds it in HBM.  C5 (B=4,
+// Ty=2500): 9.84 -> 9.07 ms/step (tools/r05_p256.sh).  The 128-channel
+// pairs measured the same here as in resblock16 (r05_p128.sh) and stay there.
 #include "conv1d_impl.h"
 
 namespace {
@@ -56,6 +64,30 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+// operand mode: 0 = split fp32 (fp32 x / y, three exact bf16 planes per
+// operand, six products), 1 = bf16 / 2 = fp16 models (16-bit x / y as the
+// 16-bit decoder holds them, one plane, one product; the gated tensor rounded
+// to the 16-bit type as the two-conv path stores it)
+template <int MODE>
+struct RpT {
+  typedef float xt;   // activation element in HBM
+  typedef __bf16 lt;  // LDS / MFMA operand element
+  static constexpr int NPL = 3;
+};
+template <>
+struct RpT<1> {
+  typedef __bf16 xt;
+  typedef __bf16 lt;
+  static constexpr int NPL = 1;
+};
+template <>
+struct RpT<2> {
+  typedef _Float16 xt;
+  typedef _Float16 lt;
+  static constexpr int NPL = 1;
+};
+__host__ __device__ constexpr int rp_npl(int mode) { return mode == 0 ? 3 : 1; }
+
 __host__ __device__ constexpr int rp_ng(int C) { return C <= 64 ? 256 : 128; }
 // threads: 4 waves (C = 64, 128), 8 waves of 64 x 64 (C = 256: 256 x 128)
 __host__ __device__ constexpr int rp_threads(int C) { return C == 256 ? 512 : 256; }
@@ -63,22 +95,36 @@ __host__ __device__ constexpr int rp_threads(int C) { return C == 256 ? 512 : 25
 // share a CU (the double-buffered chunk must fit beside nothing but the G
 // planes it aliases), 64 for the one-workgroup 256-channel tile (its X
 // buffers still fit the LDS: four slabs per barrier)
-__host__ __device__ constexpr int rp_kc(int C) { return C == 256 ? 64 : 16; }
+__host__ __device__ constexpr int rp_kc(int C, int mode = 0) {
+  return C == 256 ? 64 : 16;  // (the 16-bit mode measured the same at 32 / 64)
+}
 __host__ __device__ inline int rp_xcols(int NG, int k, int dil) {
   // NG + (k-1) dil window columns + up to 3 of alignment shift, 4-blocks
   return ((NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
 }
 // LDS: erow [2C] floats, then max(two X slab buffers, the G planes)
-__host__ __device__ inline int rp_lds_bytes(int C, int k, int dil) {
-  const int NG = rp_ng(C);
-  const int xs = 2 * 3 * rp_xcols(NG, k, dil) * (rp_kc(C) + 4);
-  const int gsz = 3 * (NG + 16) * (C / 2 + 8);
+__host__ __device__ inline int rp_lds_bytes(int C, int k, int dil, int mode = 0) {
+  const int NG = rp_ng(C), npl = rp_npl(mode);
+  const int xs = 2 * npl * rp_xcols(NG, k, dil) * (rp_kc(C, mode) + 4);
+  const int gsz = npl * (NG + 16) * (C / 2 + 8);
   return 4 * 2 * C + 2 * (xs > gsz ? xs : gsz) + 64;
 }
+// minimum waves per SIMD the kernel is compiled for (launch_bounds' second
+// argument): two 4-wave workgroups per CU below 256 channels, one 8-wave one
+// at 256.  (16-bit 256: two 8-wave workgroups per CU need <= 128 VGPRs and
+// spill 24; measured the same on C5, tools/r05_p256b.sh)
+__host__ __device__ constexpr int rp_occ(int C, int) { return C == 256 ? 1 : 2; }
 
-template <int C>
-__global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f32p_kernel(
+template <int C, int MODE = 0>
+__global__ __launch_bounds__(rp_threads(C), rp_occ(C, MODE)) void resblock_f32p_kernel(
     const RpGroup G) {
+  typedef typename RpT<MODE>::xt xt;
+  typedef typename RpT<MODE>::lt lt;
+  constexpr int NPL = RpT<MODE>::NPL;
+  typedef lt lt8 __attribute__((ext_vector_type(8)));
+  typedef lt lt4 __attribute__((ext_vector_type(4)));
+  typedef lt lt2 __attribute__((ext_vector_type(2)));
+  typedef xt xt4 __attribute__((ext_vector_type(4)));
   constexpr int H = C / 2;
   constexpr int NT = rp_threads(C);
   constexpr int WAVES_M = C >= 64 ? C / 64 : 1;
@@ -86,13 +132,14 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
   constexpr int NG = 64 * WAVES_N;
   static_assert(NG == rp_ng(C), "tile columns");
   constexpr int TM = C >= 64 ? 2 : 1, TN = 2;  // 64 x 64 per wave (C = 32: 32 x 64)
-  constexpr int KC = rp_kc(C);          // c1 channels per staged chunk
+  constexpr int KC = rp_kc(C, MODE);          // c1 channels per staged chunk
   constexpr int KCP = KC + 4;           // X chunk row pitch (bf16)
   constexpr int GP = H + 8;              // G row pitch (bf16): 16-byte rows
   constexpr int GPL = (NG + 16) * GP;    // G plane (elements)
   constexpr int S1 = C / 16, S2 = H / 16;
   constexpr int NU = ((KC / 4) * ((NG + 102) / 4) + NT - 1) / NT;  // staging units per thread
-  typedef bf16x8 av_t;
+  typedef lt8 av_t;
+  constexpr int NB = NPL == 3 ? TN : 1;  // (mid / lo B planes: split only)
 
   const int gi = (int)blockIdx.z / G.batch;
   const int b = (int)blockIdx.z - gi * G.batch;
@@ -108,7 +155,7 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
 
   extern __shared__ float smem[];
   float* const erow = smem;  // [2C]: c1 bias + cond (gate-interleaved), c2 bias
-  __bf16* const reg = reinterpret_cast<__bf16*>(smem + 2 * C);
+  lt* const reg = reinterpret_cast<lt*>(smem + 2 * C);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -151,32 +198,38 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         f32x16 c = acc[mi][ni];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bl[ni], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][mi], bh[ni], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bm[ni], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bm[ni], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bh[ni], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bh[ni], c, 0, 0, 0);
+        if constexpr (MODE == 0) {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bl[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][mi], bh[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bm[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bm[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mi], bh[ni], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bh[ni], c, 0, 0, 0);
+        } else if constexpr (MODE == 1) {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mi], bh[ni], c, 0, 0, 0);
+        } else {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][mi], bh[ni], c, 0, 0, 0);
+        }
         acc[mi][ni] = c;
       }
   };
-  // A fragments of flat step s (image [cin_pad/16][k][2][3][m_pad][8]):
+  // A fragments of flat step s (image [cin_pad/16][k][2][NPL][m_pad][8]):
   // plane q, half lhi, rows wm + mi * 32 + l32
-  auto loadA = [&](const __bf16* wl, int64_t wstep, int m_pad, int s, int total,
+  auto loadA = [&](const lt* wl, int64_t wstep, int m_pad, int s, int total,
                    av_t (*a)[TM]) {
-    const __bf16* wp = wl + (int64_t)(s < total ? s : total - 1) * wstep;
+    const lt* wp = wl + (int64_t)(s < total ? s : total - 1) * wstep;
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+    for (int q = 0; q < NPL; ++q)
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi)
         a[q][mi] = *reinterpret_cast<const av_t*>(wp + ((int64_t)q * m_pad + mi * 32) * 8);
   };
 
-  av_t a0[3][TM], a1[3][TM];
-  av_t bh0[TN], bm0[TN], bl0[TN], bh1[TN], bm1[TN], bl1[TN];
+  av_t a0[NPL][TM], a1[NPL][TM];
+  av_t bh0[TN], bm0[NB], bl0[NB], bh1[TN], bm1[NB], bl1[NB];
 
   // ---------------- phase 1: c1 over NG columns from n0 - p2 ---------------
-  const float* xb = p.x + (int64_t)b * p.x_bstride;
+  const xt* xb = reinterpret_cast<const xt*>(p.x) + (int64_t)b * p.x_bstride;
   {
     const int tw0 = n0 - p2 - p1;  // time of window column 0
     const int xstart = tw0 & ~3;   // 16-byte aligned block start
@@ -184,12 +237,12 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
     const int xcols = rp_xcols(NG, k, dil);
     const int nunits = (KC / 4) * (xcols >> 2);  // channel quads x 4-step blocks
     const int xpl = xcols * KCP;   // plane (elements)
-    __bf16* const xbuf0 = reg;
-    __bf16* const xbuf1 = reg + 3 * xpl;
+    lt* const xbuf0 = reg;
+    lt* const xbuf1 = reg + NPL * xpl;
     const float slope = p.in_slope;
     // unit u: channel quad u % (KC/4), 4-step block u / (KC/4) (a 16-lane
     // group's 8-byte LDS pieces fall on distinct banks)
-    f32x4v xr[NU][4];
+    xt4 xr[NU][4];
     int xoff[NU];
     bool xok[NU];
 #pragma unroll
@@ -201,19 +254,19 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
     }
     // loads issued unconditionally (clamped address, zeroed in lstore)
     auto gload = [&](int ch) {
-      const float* base = xb + (int64_t)ch * KC * p.x_cstride;
+      const xt* base = xb + (int64_t)ch * KC * p.x_cstride;
 #pragma unroll
       for (int q = 0; q < NU; ++q) {
         if (q * NT < nunits) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float* src = xok[q] ? base + xoff[q] + i * p.x_cstride : xb;
-            xr[q][i] = *reinterpret_cast<const f32x4v*>(src);
+            const xt* src = xok[q] ? base + xoff[q] + i * p.x_cstride : xb;
+            xr[q][i] = *reinterpret_cast<const xt4*>(src);
           }
         }
       }
     };
-    auto lstore = [&](__bf16* xs) {
+    auto lstore = [&](lt* xs) {
 #pragma unroll
       for (int q = 0; q < NU; ++q) {
         const int u = tid + NT * q;
@@ -223,39 +276,48 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float t = xr[q][i][e];
+              float t = (float)xr[q][i][e];
               t = t < 0.f ? t * slope : t;
               v[i][e] = xok[q] ? t : 0.f;
             }
-          __bf16* xh = xs + 4 * (u / (KC / 4)) * KCP + 4 * (u % (KC / 4));
+          lt* xh = xs + 4 * (u / (KC / 4)) * KCP + 4 * (u % (KC / 4));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const f32x4v w = {v[0][e], v[1][e], v[2][e], v[3][e]};
-            bf16x4 h4, m4, l4;
-            split3_bf16x4(w, h4, m4, l4);
-            *reinterpret_cast<bf16x4*>(xh + e * KCP) = h4;
-            *reinterpret_cast<bf16x4*>(xh + xpl + e * KCP) = m4;
-            *reinterpret_cast<bf16x4*>(xh + 2 * xpl + e * KCP) = l4;
+            if constexpr (NPL == 3) {
+              bf16x4 h4, m4, l4;
+              split3_bf16x4(w, h4, m4, l4);
+              *reinterpret_cast<bf16x4*>(xh + e * KCP) = h4;
+              *reinterpret_cast<bf16x4*>(xh + xpl + e * KCP) = m4;
+              *reinterpret_cast<bf16x4*>(xh + 2 * xpl + e * KCP) = l4;
+            } else {
+              lt4 w4;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) w4[i] = (lt)w[i];
+              *reinterpret_cast<lt4*>(xh + e * KCP) = w4;
+            }
           }
         }
       }
     };
     // B fragments of tap j, slab g of the chunk: rows wn + ni * 32 + l32 +
     // j * dil (+ xsh), channels 16 g + 8 lhi .. + 8 (two 8-byte reads per plane)
-    auto loadB = [&](const __bf16* xs, int j, int g, av_t* bh, av_t* bm, av_t* bl) {
+    auto loadB = [&](const lt* xs, int j, int g, av_t* bh, av_t* bm, av_t* bl) {
       const int P4 = xpl / 4;
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
-        const bf16x4* xp = reinterpret_cast<const bf16x4*>(
+        const lt4* xp = reinterpret_cast<const lt4*>(
             xs + (wn + ni * 32 + l32 + j * dil + xsh) * KCP + 16 * g + 8 * lhi);
         bh[ni] = __builtin_shufflevector(xp[0], xp[1], 0, 1, 2, 3, 4, 5, 6, 7);
-        bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
-        bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+        if constexpr (NPL == 3) {
+          bm[ni] = __builtin_shufflevector(xp[P4], xp[P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+          bl[ni] = __builtin_shufflevector(xp[2 * P4], xp[2 * P4 + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+        }
       }
     };
-    const __bf16* wl = reinterpret_cast<const __bf16*>(p.w1) +
-                       ((int64_t)(lhi * 3) * p.m_pad1 + wm + l32) * 8;
-    const int64_t wstep = (int64_t)48 * p.m_pad1;
+    const lt* wl = reinterpret_cast<const lt*>(p.w1) +
+                   ((int64_t)(lhi * NPL) * p.m_pad1 + wm + l32) * 8;
+    const int64_t wstep = (int64_t)16 * NPL * p.m_pad1;
     const int total = S1 * k;
     const int nst = (KC / 16) * k;  // k-steps per chunk: slab-major, then tap
     loadA(wl, wstep, p.m_pad1, 0, total, a0);
@@ -265,7 +327,7 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
     for (int ch = 0; ch < C / KC; ++ch) {
       const bool more = ch + 1 < C / KC;
       if (more) gload(ch + 1);  // in flight under this chunk's MFMAs
-      const __bf16* xs = (ch & 1) ? xbuf1 : xbuf0;
+      const lt* xs = (ch & 1) ? xbuf1 : xbuf0;
       const int s0 = ch * nst;
       int j = 0, g = 0;  // (tap, slab) of the next B load
       auto next = [&]() {
@@ -296,7 +358,7 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, bh0, bm0, bl0);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < NPL; ++q)
 #pragma unroll
           for (int mi = 0; mi < TM; ++mi) a0[q][mi] = a1[q][mi];
       }
@@ -306,7 +368,7 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
   }
 
   // ---------------- gate -> G planes (over the dead X buffers) -------------
-  __bf16* const gs = reg;
+  lt* const gs = reg;
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
@@ -322,41 +384,50 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
                          fast_sigmoid(acc[mi][ni][r + 1] + erow[row + 1]);
         const float g1 = fast_tanh(acc[mi][ni][r + 2] + erow[row + 2]) *
                          fast_sigmoid(acc[mi][ni][r + 3] + erow[row + 3]);
-        const f32x4v w = {in ? g0 : 0.f, in ? g1 : 0.f, 0.f, 0.f};
-        bf16x4 h4, m4, l4;
-        split3_bf16x4(w, h4, m4, l4);
-        __bf16* gp = gs + col * GP + (row >> 1);
-        *reinterpret_cast<bf16x2*>(gp) = __builtin_shufflevector(h4, h4, 0, 1);
-        *reinterpret_cast<bf16x2*>(gp + GPL) = __builtin_shufflevector(m4, m4, 0, 1);
-        *reinterpret_cast<bf16x2*>(gp + 2 * GPL) = __builtin_shufflevector(l4, l4, 0, 1);
+        lt* gp = gs + col * GP + (row >> 1);
+        if constexpr (NPL == 3) {
+          const f32x4v w = {in ? g0 : 0.f, in ? g1 : 0.f, 0.f, 0.f};
+          bf16x4 h4, m4, l4;
+          split3_bf16x4(w, h4, m4, l4);
+          *reinterpret_cast<bf16x2*>(gp) = __builtin_shufflevector(h4, h4, 0, 1);
+          *reinterpret_cast<bf16x2*>(gp + GPL) = __builtin_shufflevector(m4, m4, 0, 1);
+          *reinterpret_cast<bf16x2*>(gp + 2 * GPL) = __builtin_shufflevector(l4, l4, 0, 1);
+        } else {
+          lt2 v2;
+          v2[0] = (lt)(in ? g0 : 0.f);
+          v2[1] = (lt)(in ? g1 : 0.f);
+          *reinterpret_cast<lt2*>(gp) = v2;
+        }
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
     }
   }
   // the 16 rows past NG that phase 2's discarded columns read: zero
-  for (int i = tid; i < 3 * 16 * H; i += NT) {
+  for (int i = tid; i < NPL * 16 * H; i += NT) {
     const int pl = i / (16 * H);
     const int e = i - pl * 16 * H;
-    gs[pl * GPL + (NG + e / H) * GP + e % H] = (__bf16)0.f;
+    gs[pl * GPL + (NG + e / H) * GP + e % H] = (lt)0.f;
   }
   __syncthreads();
 
   // ---------------- phase 2: c2 from G --------------------------------------
   {
-    const __bf16* wl = reinterpret_cast<const __bf16*>(p.w2) +
-                       ((int64_t)(lhi * 3) * p.m_pad2 + wm + l32) * 8;
-    const int64_t wstep = (int64_t)48 * p.m_pad2;
+    const lt* wl = reinterpret_cast<const lt*>(p.w2) +
+                   ((int64_t)(lhi * NPL) * p.m_pad2 + wm + l32) * 8;
+    const int64_t wstep = (int64_t)16 * NPL * p.m_pad2;
     const int total = S2 * k;
-    const __bf16* gl = gs + (wn + l32) * GP + 8 * lhi;
+    const lt* gl = gs + (wn + l32) * GP + 8 * lhi;
     int j = 0, g = 0;  // tap / slab of the next B load
     auto loadB = [&](av_t* bh, av_t* bm, av_t* bl) {
-      const __bf16* x = gl + j * GP + 16 * g;
+      const lt* x = gl + j * GP + 16 * g;
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         bh[ni] = *reinterpret_cast<const av_t*>(x + ni * 32 * GP);
-        bm[ni] = *reinterpret_cast<const av_t*>(x + ni * 32 * GP + GPL);
-        bl[ni] = *reinterpret_cast<const av_t*>(x + ni * 32 * GP + 2 * GPL);
+        if constexpr (NPL == 3) {
+          bm[ni] = *reinterpret_cast<const av_t*>(x + ni * 32 * GP + GPL);
+          bl[ni] = *reinterpret_cast<const av_t*>(x + ni * 32 * GP + 2 * GPL);
+        }
       }
       if (++j == k) {
         j = 0;
@@ -383,7 +454,7 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
 
   // residual (+ accumulate / branch-mean division) epilogue, as the conv's
   // single-output STORE: every load of a 32 x 32 sub-tile issued first
-  float* const yb = p.y + (int64_t)b * p.y_bstride;
+  xt* const yb = reinterpret_cast<xt*>(p.y) + (int64_t)b * p.y_bstride;
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
@@ -396,13 +467,13 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = wm + mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
-        rv[r] = xb[(int64_t)row * p.x_cstride + tc];
+        rv[r] = (float)xb[(int64_t)row * p.x_cstride + tc];
       }
       if (p.accumulate) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = wm + mi * 32 + 4 * lhi + (r & 3) + 8 * (r >> 2);
-          yo[r] = yb[(int64_t)row * p.y_cstride + tc];
+          yo[r] = (float)yb[(int64_t)row * p.y_cstride + tc];
         }
       }
       if (st) {
@@ -413,31 +484,31 @@ __global__ __launch_bounds__(rp_threads(C), 512 / rp_threads(C)) void resblock_f
           float o = rv[r] + v;  // (the conv's rv + res_scale * v, res_scale 1)
           if (p.accumulate) o = yo[r] + o;
           if (p.post_div != 1.0f) o = o / p.post_div;
-          yb[(int64_t)row * p.y_cstride + t] = t < L ? o : 0.f;
+          yb[(int64_t)row * p.y_cstride + t] = (xt)(t < L ? o : 0.f);
         }
       }
     }
   }
 }
 
-template <int C>
+template <int C, int MODE = 0>
 int rp_launch(const RpGroup& g, hipStream_t s) {
   int lds = 0, gx = 0;
   for (int i = 0; i < g.n; ++i) {
     const vits_resblock_pair_desc& d = g.d[i];
-    const int l = rp_lds_bytes(C, d.k, d.dil);
+    const int l = rp_lds_bytes(C, d.k, d.dil, MODE);
     if (l > lds) lds = l;
     const int BN = rp_ng(C) - (d.k - 1);
     const int x = (d.t_len + BN - 1) / BN;
     if (x > gx) gx = x;
   }
   if (lds > 160 * 1024) return VITS_E_UNSUP;
-  hipLaunchKernelGGL((resblock_f32p_kernel<C>), dim3(gx, 1, g.n * g.batch), dim3(rp_threads(C)), lds,
-                     s, g);
+  hipLaunchKernelGGL((resblock_f32p_kernel<C, MODE>), dim3(gx, 1, g.n * g.batch),
+                     dim3(rp_threads(C)), lds, s, g);
   return vits_launch_status();
 }
 
-int rp_check(const vits_resblock_pair_desc& d) {
+int rp_check(const vits_resblock_pair_desc& d, int mode = 0) {
   VITS_CHECK_ARG(d.x && d.w1 && d.w2 && d.y);
   // other workgroups still read x (halos, residual): never write in place
   VITS_CHECK_ARG(reinterpret_cast<const void*>(d.y) != reinterpret_cast<const void*>(d.x));
@@ -449,10 +520,11 @@ int rp_check(const vits_resblock_pair_desc& d) {
   VITS_CHECK_SHAPE(d.m_pad1 >= d.channels && d.m_pad2 >= d.channels && (d.m_pad1 & 3) == 0 &&
                    (d.m_pad2 & 3) == 0);
   VITS_CHECK_SHAPE(d.cin_pad1 >= d.channels && d.cin_pad2 >= d.channels / 2);
-  // 16-byte x staging: fp32 time-contiguous rows, T % 4 == 0, aligned
+  // 4-step x staging (16 bytes fp32 / 8 bytes 16-bit): time-contiguous rows,
+  // T % 4 == 0, aligned
   VITS_CHECK_SHAPE((d.t_len & 3) == 0 && (d.x_cstride & 3) == 0 && (d.x_bstride & 3) == 0 &&
                    d.x_cstride >= d.t_len && d.y_cstride >= d.t_len &&
-                   (reinterpret_cast<uintptr_t>(d.x) & 15) == 0);
+                   (reinterpret_cast<uintptr_t>(d.x) & (mode ? 7 : 15)) == 0);
   // 32-bit staging offsets within one utterance
   VITS_CHECK_SHAPE((int64_t)d.channels * d.x_cstride < (1LL << 31));
   VITS_CHECK_SHAPE((reinterpret_cast<uintptr_t>(d.w1) & 15) == 0 &&
@@ -461,6 +533,27 @@ int rp_check(const vits_resblock_pair_desc& d) {
 }
 
 }  // namespace
+
+// the 16-bit models' 256-channel pairs (vits_resblock_pair16_forward routes
+// them here: resblock16.hip stages whole windows, which a 256-channel window
+// does not fit)
+int vits_rp16_256(const vits_resblock_pair_desc* d, int n, int batch, int wdtype,
+                  hipStream_t s) {
+  if (!d || n < 1 || n > RP_GROUP || batch < 1) return VITS_E_ARG;
+  if (wdtype != VITS_WDT_BF16 && wdtype != VITS_WDT_F16) return VITS_E_ARG;
+  const int mode = wdtype == VITS_WDT_BF16 ? 1 : 2;
+  RpGroup g;
+  g.n = n;
+  g.batch = batch;
+  for (int i = 0; i < n; ++i) {
+    const int rc = rp_check(d[i], mode);
+    if (rc) return rc;
+    if (d[i].channels != d[0].channels) return VITS_E_SHAPE;
+    g.d[i] = d[i];
+  }
+  if (d[0].channels != 256) return VITS_E_SHAPE;
+  return mode == 1 ? rp_launch<256, 1>(g, s) : rp_launch<256, 2>(g, s);
+}
 
 extern "C" int vits_resblock_pair_f32p_forward(const vits_resblock_pair_desc* d, int n, int batch,
                                                void* stream) {

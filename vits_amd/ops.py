@@ -703,15 +703,21 @@ def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch
 # fused pairs of 16-bit models (csrc/resblock16.hip): VITS_FUSED_PAIRS16=0
 # keeps their two-conv path
 FUSED_PAIRS16 = True
+# largest k fused on the 256-channel stage (resblock_f32p.hip's 16-bit mode;
+# 0 = none, the two-conv path)
+PAIR16_256_MAX_K = 15
 
 
 def resblock_pair16_supported(c1: PackedConv, c2: PackedConv, x: torch.Tensor) -> bool:
     """Pairs of a 16-bit model with 16-bit activations that run fused
-    (csrc/resblock16.hip): the 32- and 64-channel stages, any odd k with
-    (k - 1) * dil <= 96, 8-byte aligned time rows (T % 4 == 0)."""
+    (csrc/resblock16.hip; the 256-channel stage csrc/resblock_f32p.hip),
+    any odd k with (k - 1) * dil <= 96, 8-byte aligned time rows
+    (T % 4 == 0)."""
     C_ = c2.out_channels
+    if C_ == 256 and c1.k > PAIR16_256_MAX_K:
+        return False
     return (FUSED_PAIRS16 and c1.wdtype in (WDT_BF16, WDT_F16) and c2.wdtype == c1.wdtype
-            and x.dtype == _WDT_TORCH[c1.wdtype] and C_ in (32, 64, 128) and c1.m == C_
+            and x.dtype == _WDT_TORCH[c1.wdtype] and C_ in (32, 64, 128, 256) and c1.m == C_
             and c1.cin == C_ and c2.cin == C_ // 2 and c2.m == C_ and c1.k == c2.k
             and c1.k % 2 == 1 and (c1.k - 1) * c1.dil <= 96 and c2.dil == 1
             and c1.epi == EPI_GATE and x.shape[2] % 4 == 0 and x.stride(2) == 1
