@@ -1,0 +1,18 @@
+#!/bin/bash
+# GA conv A-prefetch ring depth (GA_PF 4 = default build, 1 = one step ahead
+# as before, 2): 16-bit kernel / model tests on the default build, then the
+# C5 per-dispatch trace and the C5 leg per arm
+set -e
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_configs_gpu.py tests/test_models_gpu.py -k "bf16 or f16 or lowp or 16 or c5" > gpurun_out/r05_gapf_tests.txt 2>&1
+for L in default pf1 pf2; do
+  if [ $L = default ]; then unset VITS_AMD_LIB; else export VITS_AMD_LIB=vits_amd/lib/ab_$L.so; fi
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lfg_$L -o run -- python3 tools/longform_pmc.py --replays 3 > gpurun_out/lfg_$L.log 2>&1
+done
+for r in 1 2; do
+for L in default pf1 pf2; do
+  if [ $L = default ]; then unset VITS_AMD_LIB; else export VITS_AMD_LIB=vits_amd/lib/ab_$L.so; fi
+  timeout -k 10 240 python -u tools/ab_legs.py --legs longform 2>/dev/null >> gpurun_out/r05_gapf_ab.txt
+done
+done

@@ -618,6 +618,89 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
           acc[mi][ni] = c;
         }
     };
+#ifndef GA_PF
+#define GA_PF 4
+#endif
+    if constexpr (!SPL && GA_PF > 1 && V4 && BN <= 128) {
+      // GA: one MFMA per fragment pair leaves TM * TN MFMAs (~128 cycles)
+      // between a step's A load and its use - less than an L2 round trip.
+      // The A fragments run PF - 1 steps ahead in a register ring instead
+      // (ring slot = step % PF within a chunk; the chunk's last nst % PF
+      // steps leave the ring rotated, which a switch undoes).  C5 trace
+      // (profiles/r05_gapf_*): WN in_layer convs 714 -> 672 us, upsamplers
+      // 716 -> 700 us per step.  Only the 16-byte-staged 128-column tiles:
+      // the element-staged and 256-column ones reach 168 VGPRs and spill.
+      constexpr int PF = GA_PF > 1 ? GA_PF : 2;  // (GA_PF = 1: the branch below)
+      static_assert(PF == 2 || PF == 4, "ring parity");
+      av_t ar[PF][1][TM];
+      av_t bb[2][TN];
+#pragma unroll
+      for (int i = 0; i < PF - 1; ++i) loadA(i, ar[i]);
+      gload(0);
+      lstore(xbuf1, 0);
+      __syncthreads();
+      for (int ch = 0; ch < nchunks; ++ch) {
+        const bool more = ch + 1 < nchunks;
+        if (more) gload((ch + 1) * kc);  // in flight under this chunk's MFMAs
+        const int buf = ch & 1;
+        const int s0 = ch * nst;
+        int j = 0, g = 0;
+        auto next = [&]() {
+          if (++j == k) {
+            j = 0;
+            ++g;
+          }
+        };
+        loadB(buf, 0, 0, bb[0], nullptr, nullptr);
+        int st = 0;
+        for (; st + PF <= nst; st += PF) {
+#pragma unroll
+          for (int u = 0; u < PF; ++u) {
+            loadA(s0 + st + u + PF - 1, ar[(u + PF - 1) % PF]);
+            next();
+            if (st + u + 1 < nst) loadB(buf, j, g, bb[(u + 1) & 1], nullptr, nullptr);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(ar[u], bb[u & 1], nullptr, nullptr);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        const int r = nst - st;  // 0 .. PF - 1 steps left
+#pragma unroll
+        for (int u = 0; u < PF - 1; ++u) {
+          if (u < r) {
+            loadA(s0 + st + u + PF - 1, ar[(u + PF - 1) % PF]);
+            next();
+            if (st + u + 1 < nst) loadB(buf, j, g, bb[(u + 1) & 1], nullptr, nullptr);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(ar[u], bb[u & 1], nullptr, nullptr);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        // the next chunk's first PF - 1 steps sit in slots r .. r + PF - 2
+        // (mod PF): move them to 0 .. PF - 2
+        auto rot = [&](auto R) {
+          constexpr int rr = decltype(R)::value;
+          av_t t[PF - 1][TM];
+#pragma unroll
+          for (int i = 0; i < PF - 1; ++i)
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) t[i][mi] = ar[(i + rr) % PF][0][mi];
+#pragma unroll
+          for (int i = 0; i < PF - 1; ++i)
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi) ar[i][0][mi] = t[i][mi];
+        };
+        if (r == 1) rot(std::integral_constant<int, 1>());
+        if constexpr (PF > 2) {
+          if (r == 2) rot(std::integral_constant<int, 2>());
+        }
+        if constexpr (PF > 3) {
+          if (r == 3) rot(std::integral_constant<int, 3>());
+        }
+        if (more) lstore(buf ? xbuf1 : xbuf2, (ch + 1) * kc);
+        __syncthreads();
+      }
+    } else {
     av_t a0[NPL][TM], a1[NPL][TM];
     av_t bh0[TN], bm0[NB], bl0[NB], bh1[TN], bm1[NB], bl1[NB];
     loadA(0, a0);
@@ -669,6 +752,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
       if (more) lstore(buf ? xbuf1 : xbuf2, (ch + 1) * kc);
       __syncthreads();
     }
+    }  // (GA ring / one step ahead)
   } else {
 
   if constexpr (WPS)
@@ -1029,6 +1113,9 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
             const int t = n * u + ph - p.up_pad;
             if (t >= 0 && t < p.t_out) {
               const float v = acc[mi][ni][r] + erow[rloc + ro];
+#ifdef UP_STORE_PROBE
+              if (v != v)
+#endif
               store_std<io_t>(o0, b, oc, t, v, t >= len_b);
             }
           }
