@@ -1,0 +1,17 @@
+#!/bin/bash
+# resblock16 A-fragment ring (R16_PF 4 = default build, 2 = one step ahead as
+# before): 16-bit pair / model tests, then the C5 trace and leg per arm
+set -e
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_configs_gpu.py tests/test_models_gpu.py -k "bf16 or f16 or lowp or 16 or c5" > gpurun_out/r05_r16pf_tests.txt 2>&1
+for L in default r16pf2; do
+  if [ $L = default ]; then unset VITS_AMD_LIB; else export VITS_AMD_LIB=vits_amd/lib/ab_$L.so; fi
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lfr_$L -o run -- python3 tools/longform_pmc.py --replays 3 > gpurun_out/lfr_$L.log 2>&1
+done
+for r in 1 2; do
+for L in default r16pf2; do
+  if [ $L = default ]; then unset VITS_AMD_LIB; else export VITS_AMD_LIB=vits_amd/lib/ab_$L.so; fi
+  timeout -k 10 240 python -u tools/ab_legs.py --legs longform 2>/dev/null >> gpurun_out/r05_r16pf_ab.txt
+done
+done

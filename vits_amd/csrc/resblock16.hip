@@ -37,6 +37,9 @@
 namespace {
 
 constexpr int R16_GROUP = 3;
+#ifndef R16_PF
+#define R16_PF 4  // A-fragment ring depth (2: one step ahead)
+#endif
 // phase-1 columns per tile: 256 for C = 32 / 64 (4 waves x 64 columns),
 // 128 for C = 128 (2 x 2 waves of 64 rows x 64 columns: the 128-channel
 // window and gated tile fit two workgroups per CU)
@@ -66,13 +69,22 @@ __host__ __device__ inline int r16_xcols(int NG, int k, int dil) {
   // NG + (k-1) dil window columns + up to 3 of alignment shift, 4-blocks
   return ((NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
 }
+#ifndef R16_ALIAS
+#define R16_ALIAS 1
+#endif
+// the gated tile G overlays the c1 window (dead after phase 1; one barrier
+// between): 50 KB instead of 71 KB at C = 128, k = 11 - three workgroups per
+// CU instead of two on the 64- and 128-channel stages (C5 trace: this kernel
+// family 4.95 -> 4.82 ms per step, profiles/r05_r16al_*)
 __host__ __device__ inline int r16_lds_bytes(int C, int k, int dil) {
   const int xp = C + 8, gp = C / 2 + 8, NG = r16_ng(C);
-  return 2 * (r16_xcols(NG, k, dil) * xp + (NG + 16) * gp) + 4 * 2 * C + 64;
+  const int xsz = r16_xcols(NG, k, dil) * xp, gsz = (NG + 16) * gp;
+  return 2 * (R16_ALIAS ? (xsz > gsz ? xsz : gsz) : xsz + gsz) + 4 * 2 * C + 64;
 }
 
 template <int C, typename T, bool MEAN>
-__global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
+__global__ __launch_bounds__(256, (MEAN || !R16_ALIAS) ? 2 : 3) void resblock16_kernel(
+    const R16Group G) {
   constexpr int H = C / 2;
   constexpr int NG = r16_ng(C);
   constexpr int WAVES_M = C == 128 ? 2 : 1;
@@ -129,7 +141,7 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
   const int p1 = (k - 1) * dil / 2;
   const int p2 = (k - 1) / 2;
   const int xcols = r16_xcols(NG, k, dil);
-  T* const gs = xs + xcols * XP;                              // [NG + 16][GP]
+  T* const gs = R16_ALIAS ? xs : xs + xcols * XP;              // [NG + 16][GP]
   if (mem > 0) __syncthreads();  // the previous member's reads of LDS are done
 
   // row constants: c1 bias + cond (gate-interleaved order), c2 bias
@@ -241,27 +253,41 @@ __global__ __launch_bounds__(256, 2) void resblock16_kernel(const R16Group G) {
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma(a[mi], bb[ni], acc[mi][ni]);
     };
-    t8 a0[TM], b0[TN], a1[TM], b1[TN];
-    loadA(0, a0);
-    loadB(b0);
+    // A fragments PF - 1 steps ahead in a register ring (slot = step % PF):
+    // one step of TM * TN MFMAs does not cover an L2 round trip.  C5 trace:
+    // this kernel family 4.94 -> 4.84 ms per step (profiles/r05_r16pf_*)
+    constexpr int PF = R16_PF;
+    static_assert(PF == 2 || PF == 4, "ring parity");
+    t8 ar[PF][TM], bb[2][TN];
+#pragma unroll
+    for (int i = 0; i < PF - 1; ++i) loadA(i, ar[i]);
+    loadB(bb[0]);
     int s = 0;
-    for (; s + 2 <= nsteps; s += 2) {
-      loadA(s + 1, a1);
-      loadB(b1);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      loadA(s + 2, a0);
-      if (s + 2 < nsteps) loadB(b0);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(a1, b1);
-      __builtin_amdgcn_sched_barrier(0);
+    for (; s + PF <= nsteps; s += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        loadA(s + u + PF - 1, ar[(u + PF - 1) % PF]);
+        if (s + u + 1 < nsteps) loadB(bb[(u + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(ar[u], bb[u & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-    if (s < nsteps) mma(a0, b0);
+    // the last nsteps % PF steps: their A fragments are already in slots 0..
+#pragma unroll
+    for (int u = 0; u < PF - 1; ++u) {
+      if (s + u < nsteps) {
+        if (s + u + 1 < nsteps) loadB(bb[(u + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(ar[u], bb[u & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   };
 
   // ---------------- phase 1: c1 over NG columns from n0 - p2 ---------------
   gemm(reinterpret_cast<const T*>(p.w1), p.m_pad1, S1 * k, xs, XP, wn + xsh, dil);
+  if (R16_ALIAS) __syncthreads();  // every wave's window reads are done: G overlays it
 
   // gate epilogue -> G (zero outside [0, L)); the 16 columns past NG that
   // phase 2's discarded columns read are zeroed too
