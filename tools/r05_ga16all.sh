@@ -1,6 +1,7 @@
 #!/bin/bash
 # every inference 16-bit conv group on the GA path (GA16_ALL) vs the k >= 5
 # rule: C5 trace + leg per arm, after the 16-bit tests on the variant
+# (the GA16_ALL switch in conv1d.hip::ga16 was removed after this measurement)
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
