@@ -1064,6 +1064,58 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   }
   __syncthreads();
 
+#ifndef UP_LDS
+#define UP_LDS 1
+#endif
+  if constexpr (EPI == VITS_EPI_UPSAMPLE && UP_LDS) {
+    // Polyphase output row = oc * u + phase lands at time n * u + phase - pad:
+    // stored from the MFMA layout, each store instruction writes 32 samples
+    // at stride u (C5 probe: 160 us of the four upsamplers' 716 per step).
+    // A plain store (no act / residual / accumulate / division - every
+    // upsampler) goes through LDS instead: the tile [BM][BN + 2] (io_t, the
+    // value rounded once, as st_io does), then each channel's contiguous run
+    // of BN * u samples with consecutive threads on consecutive samples.
+    // C5 trace: the four upsamplers 729 -> 657 us per step; headline
+    // 20.16 -> 20.03 ms (profiles/r05_uplds_*).
+    if (o0.act == VITS_ACT_NONE && !o0.res && !o0.accumulate && o0.post_div == 1.0f) {
+      constexpr int TP = BN + 2;
+      io_t* const tile = reinterpret_cast<io_t*>(smem + BM);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+          const int col = wn + ni * 32 + l32;
+          const int rloc = wm + mi * 32 + 4 * lhi;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ro = rloc + (r & 3) + 8 * (r >> 2);
+            tile[ro * TP + col] = (io_t)(acc[mi][ni][r] + erow[ro]);
+          }
+        }
+      __syncthreads();
+      const int u = p.up_u;
+      const float inv_u = 1.0f / (float)u;  // (exact floor for j < 2^14, u <= 64)
+      const int oc0 = m0 / u;
+      const int oc1 = min((m0 + BM - 1) / u, p.m / u - 1);
+      const int span = BN * u;
+      const int tb = n0 * u - p.up_pad;  // time of j = 0
+      io_t* const yb = reinterpret_cast<io_t*>(o0.y) + (int64_t)b * o0.y_bstride;
+      for (int oc = oc0; oc <= oc1; ++oc) {
+        io_t* const yc = yb + (int64_t)oc * o0.y_cstride;
+        const int rb = oc * u - m0;  // tile row of phase 0
+        for (int j = tid; j < span; j += 256) {
+          const int nl = (int)(((float)j + 0.5f) * inv_u);
+          const int ph = j - nl * u;
+          const int rl = rb + ph;
+          const int t = tb + j;
+          if (rl >= 0 && rl < BM && n0 + nl < p.n_out && t >= 0 && t < p.t_out)
+            yc[t] = t >= len_b ? (io_t)0.f : tile[rl * TP + nl];
+        }
+      }
+      return;
+    }
+  }
+
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
@@ -1278,7 +1330,10 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
                             : 2 * (size_t)d.k * BM + 2 * xrs[i] + 64;
     // (WG: two X buffers, no W)
     const size_t tail_wg = WG && !SPL ? (size_t)(d.dil + 2) * (d.kc + 4) / 2 + 64 : tail;
-    const size_t l = sizeof(float) * (wst + ((SPL && !WG) ? 1 : 2) * xslots + tail_wg);
+    size_t l = sizeof(float) * (wst + ((SPL && !WG) ? 1 : 2) * xslots + tail_wg);
+    // UPSAMPLE: the output tile staged after the row constants (UP_LDS)
+    const size_t lup = sizeof(float) * BM + (size_t)BM * (BN + 2) * (IO16 ? 2 : 4) + 64;
+    if (UP_LDS && d.epi == VITS_EPI_UPSAMPLE && lup > l) l = lup;
     if (l > lds) lds = l;
     const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;
     if (x > gx) gx = x;
