@@ -565,10 +565,12 @@ def fp32_arith() -> str:
         return "exact: v_mfma_f32_32x32x2_f32 (bitwise an fp32 fma chain)"
     from vits_amd import ops
 
-    return (f"split: convs with >= {ops._f32s_min_rows()} GEMM rows split each fp32 operand "
-            "exactly into three bf16 terms (weights pre-split into planes), six bf16 MFMAs per "
-            "product, fp32 accumulation (error vs fp64 at or below the exact-f32 kernel's, "
-            "tests/test_kernels_gpu.py); the 32-channel stage exact f32")
+    return (f"split: convs with >= {ops._f32s_min_rows()} GEMM rows, and every fused ResBlock2 "
+            "pair (the 32-channel stage included), split each fp32 operand exactly into three "
+            "bf16 terms (weights pre-split into planes), six bf16 MFMAs per product, fp32 "
+            "accumulation (error vs fp64 at or below the exact-f32 kernel's, "
+            "tests/test_kernels_gpu.py): every conv / pair launch of the headline step; conv_post "
+            "+ tanh (1 output row) is its own fp32 FMA kernel")
 
 
 def _launch_ranks(args) -> int:

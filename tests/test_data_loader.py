@@ -160,3 +160,21 @@ def test_wav_header_any_pcm_width(tmp_path):
     p = tmp_path / "c.wav"
     p.write_bytes(riff)
     assert _wav_header(str(p)) == (16000, n)
+
+
+def test_wav_header_truncated_or_placeholder_size(tmp_path):
+    """A data chunk whose header size is larger than the file (truncated) or
+    a streaming placeholder (0 / 0xFFFFFFFF) is counted from the bytes that
+    are actually there."""
+    import struct
+
+    from vits_amd.data_utils import _wav_header
+
+    fmt = struct.pack("<HHIIHH", 1, 1, 16000, 32000, 2, 16)
+    pcm = b"\1\0" * 500
+    for declared in (0, 0xFFFFFFFF, 2 * 900):
+        riff = (b"RIFF" + struct.pack("<I", 0) + b"WAVE" + b"fmt " + struct.pack("<I", len(fmt))
+                + fmt + b"data" + struct.pack("<I", declared) + pcm)
+        p = tmp_path / f"t{declared}.wav"
+        p.write_bytes(riff)
+        assert _wav_header(str(p)) == (16000, 500), declared

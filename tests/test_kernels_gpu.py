@@ -675,7 +675,7 @@ def test_resblock_pair_f32p_fused(device, monkeypatch, C, k, dil, T):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_generator16_fused_pairs_match_two_conv_path(device, monkeypatch, dt):
     """A 16-bit model's Generator with resblock16 pairs on its 32/64-channel
-    stages against its two-conv path (VITS_FUSED_PAIRS16=0): the same
+    stages against its two-conv path (ops.FUSED_PAIRS16 = False): the same
     rounding points (16-bit gated tensor, one rounding of each output), only
     the fp32 accumulation order differs - 1e-2 (bf16) / 2e-3 (fp16) of the
     waveform magnitude."""
@@ -697,7 +697,7 @@ def test_generator16_fused_pairs_match_two_conv_path(device, monkeypatch, dt):
 
 def test_generator_fused_pairs_match_two_conv_path(device, monkeypatch):
     """The Generator with fused pairs on its 32/64-channel stages equals the
-    two-conv path (VITS_FUSED_PAIRS=0) to fp32 rounding."""
+    two-conv path (engine._FUSED_PAIRS = False) to fp32 rounding."""
     from common import base_model
     from vits_amd import engine
 

@@ -27,7 +27,7 @@ def _device_select(words: np.ndarray, high: int):
     for i, w in enumerate(words.view(np.uint32)):
         if (int(w) & mask) <= rng:
             return int(w) & mask, i + 1
-    return 0, -1
+    return 0, -2  # every word of the pool rejected: the host advances and retries
 
 
 def test_device_draw_reproduces_numpy_randint_and_state():
@@ -52,3 +52,38 @@ def test_device_draw_rejects_slices_that_do_not_fit():
     pool, state = ops.numpy_draw_pool()
     assert _device_select(pool, 0)[1] == -1
     assert _device_select(pool, -5)[1] == -1
+
+
+def _host_draw(high: int, n: int):
+    """infer.py EmoVITS._infer_graph's draw protocol (vits_amd/infer.py:200-214)
+    with a pool of ``n`` words: -2 (all rejected) advances numpy's generator
+    past the pool and draws again from the next words."""
+    while True:
+        pool, state = ops.numpy_draw_pool(n)
+        start, used = _device_select(pool, high)
+        if used == -2:
+            ops.numpy_draw_commit(state, n)
+            continue
+        assert used >= 0
+        ops.numpy_draw_commit(state, used)
+        return start
+
+
+def test_device_draw_all_rejected_pool_retries_in_step_with_numpy():
+    """Pools of 1-3 words at ranges whose masked rejection rate is ~1/2, so
+    whole pools are rejected often: the retry must still give randint's value
+    and leave the generator where randint leaves it."""
+    retries = 0
+    for seed in range(60):
+        for high in (2 ** 31 + 1, 2 ** 16 + 1, 5):
+            for n in (1, 2, 3):
+                np.random.seed(seed)
+                want = np.random.randint(high)
+                want_next = np.random.randint(1 << 30)
+                np.random.seed(seed)
+                pool, _ = ops.numpy_draw_pool(n)
+                retries += _device_select(pool, high)[1] == -2
+                np.random.seed(seed)
+                assert _host_draw(high, n) == want, (seed, high, n)
+                assert np.random.randint(1 << 30) == want_next, (seed, high, n)
+    assert retries > 20  # the -2 branch was exercised

@@ -307,6 +307,57 @@ def test_bucketed_allreduce_equals_flat_allreduce(tmp_path):
     assert np.array_equal(res["allreduce"], res["flat"])
 
 
+class _RecordingDist:
+    """Stand-in for torch.distributed in _GradBuckets' CPU path: records the
+    size of every all-reduced flat buffer (world size 1)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def all_reduce(self, t):
+        self.calls.append(t.numel())
+
+    def get_world_size(self):
+        return 1
+
+
+def test_grad_buckets_launch_in_index_order(monkeypatch):
+    """Buckets whose gradients complete out of order are all-reduced in
+    bucket-index order (collectives pair up across ranks), and a parameter
+    without a gradient is zero-filled so every rank's bucket layout agrees."""
+    from vits_amd import train as T
+
+    rec = _RecordingDist()
+    monkeypatch.setattr(T, "dist", rec)
+    net = torch.nn.Module()
+    net.a = torch.nn.Linear(3, 2)        # bucket 0: 8 elements
+    net.b = torch.nn.Linear(4, 4)        # bucket 1: 20 elements
+    net.c = torch.nn.Linear(1, 1, bias=False)  # bucket 2: 1 element, never gets a gradient
+    gb = T._GradBuckets(net, (("a.",), ("b.",), ("",)), torch.device("cpu"))
+    assert [sum(p.numel() for p in b) for b in gb.buckets] == [8, 20, 1]
+    gb.begin()
+    net.b(torch.randn(2, 4)).sum().backward()  # bucket 1 completes first
+    assert rec.calls == []                     # ... but waits for bucket 0
+    net.a(torch.randn(2, 3)).sum().backward()
+    assert rec.calls == [8, 20]
+    gb.finish()                                # bucket 2: no gradient -> zeros
+    assert rec.calls == [8, 20, 1]
+    assert torch.equal(net.c.weight.grad, torch.zeros_like(net.c.weight))
+
+
+def test_g_buckets_cover_every_parameter_within_50mb():
+    """G_BUCKETS at configs/base.json: every G parameter in exactly one
+    bucket (the first matching), each bucket <= 50 MB of fp32 gradients."""
+    from vits_amd.train import G_BUCKETS, _bucket_of, build_models, default_hps
+
+    net_g, _ = build_models(default_hps(), torch.device("cpu"))
+    sizes = [0] * len(G_BUCKETS)
+    for n, p in net_g.named_parameters():
+        sizes[_bucket_of(n, G_BUCKETS)] += 4 * p.numel()
+    assert all(0 < s <= 50e6 for s in sizes), sizes
+    assert sum(sizes) == 4 * sum(p.numel() for p in net_g.parameters())
+
+
 @pytest.mark.gpu
 def test_train_step_gpu_fp16(device):
     hps = tiny_hps()

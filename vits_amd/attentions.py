@@ -17,7 +17,7 @@ from .modules import LayerNorm
 
 
 # self-attention's q / k / v projections as one HIP conv under autocast
-# (train_ops.conv1d_cat); VITS_QKV_CAT=0 keeps three
+# (train_ops.conv1d_cat); False (tests) keeps three
 QKV_CAT = True
 
 

@@ -7,11 +7,7 @@
 
 #include "common.h"
 
-#ifdef VITS_NOPRIO
-#define VITS_PRIO(x) ((void)0)
-#else
 #define VITS_PRIO(x) __builtin_amdgcn_s_setprio(x)
-#endif
 
 namespace vits_conv {
 
@@ -618,10 +614,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
           acc[mi][ni] = c;
         }
     };
-#ifndef GA_PF
-#define GA_PF 4
-#endif
-    if constexpr (!SPL && GA_PF > 1 && V4 && BN <= 128) {
+    if constexpr (!SPL && V4 && BN <= 128) {
       // GA: one MFMA per fragment pair leaves TM * TN MFMAs (~128 cycles)
       // between a step's A load and its use - less than an L2 round trip.
       // The A fragments run PF - 1 steps ahead in a register ring instead
@@ -630,7 +623,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
       // (profiles/r05_gapf_*): WN in_layer convs 714 -> 672 us, upsamplers
       // 716 -> 700 us per step.  Only the 16-byte-staged 128-column tiles:
       // the element-staged and 256-column ones reach 168 VGPRs and spill.
-      constexpr int PF = GA_PF > 1 ? GA_PF : 2;  // (GA_PF = 1: the branch below)
+      constexpr int PF = 4;
       static_assert(PF == 2 || PF == 4, "ring parity");
       av_t ar[PF][1][TM];
       av_t bb[2][TN];
@@ -1064,10 +1057,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
   }
   __syncthreads();
 
-#ifndef UP_LDS
-#define UP_LDS 1
-#endif
-  if constexpr (EPI == VITS_EPI_UPSAMPLE && UP_LDS) {
+  if constexpr (EPI == VITS_EPI_UPSAMPLE) {
     // Polyphase output row = oc * u + phase lands at time n * u + phase - pad:
     // stored from the MFMA layout, each store instruction writes 32 samples
     // at stride u (C5 probe: 160 us of the four upsamplers' 716 per step).
@@ -1165,9 +1155,6 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
             const int t = n * u + ph - p.up_pad;
             if (t >= 0 && t < p.t_out) {
               const float v = acc[mi][ni][r] + erow[rloc + ro];
-#ifdef UP_STORE_PROBE
-              if (v != v)
-#endif
               store_std<io_t>(o0, b, oc, t, v, t >= len_b);
             }
           }
@@ -1331,9 +1318,9 @@ int launch_tile_v(const ConvGroup& g, hipStream_t s, const size_t* xrs) {
     // (WG: two X buffers, no W)
     const size_t tail_wg = WG && !SPL ? (size_t)(d.dil + 2) * (d.kc + 4) / 2 + 64 : tail;
     size_t l = sizeof(float) * (wst + ((SPL && !WG) ? 1 : 2) * xslots + tail_wg);
-    // UPSAMPLE: the output tile staged after the row constants (UP_LDS)
+    // UPSAMPLE: the output tile staged after the row constants
     const size_t lup = sizeof(float) * BM + (size_t)BM * (BN + 2) * (IO16 ? 2 : 4) + 64;
-    if (UP_LDS && d.epi == VITS_EPI_UPSAMPLE && lup > l) l = lup;
+    if (d.epi == VITS_EPI_UPSAMPLE && lup > l) l = lup;
     if (l > lds) lds = l;
     const int x = (d.n_out + BN - 1) / BN, y = (d.m + BM - 1) / BM;
     if (x > gx) gx = x;

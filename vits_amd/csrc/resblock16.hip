@@ -37,9 +37,6 @@
 namespace {
 
 constexpr int R16_GROUP = 3;
-#ifndef R16_PF
-#define R16_PF 4  // A-fragment ring depth (2: one step ahead)
-#endif
 // phase-1 columns per tile: 256 for C = 32 / 64 (4 waves x 64 columns),
 // 128 for C = 128 (2 x 2 waves of 64 rows x 64 columns: the 128-channel
 // window and gated tile fit two workgroups per CU)
@@ -69,9 +66,6 @@ __host__ __device__ inline int r16_xcols(int NG, int k, int dil) {
   // NG + (k-1) dil window columns + up to 3 of alignment shift, 4-blocks
   return ((NG + (k - 1) * dil + 3 + 3) >> 2) << 2;
 }
-#ifndef R16_ALIAS
-#define R16_ALIAS 1
-#endif
 // the gated tile G overlays the c1 window (dead after phase 1; one barrier
 // between): 50 KB instead of 71 KB at C = 128, k = 11 - three workgroups per
 // CU instead of two on the 64- and 128-channel stages (C5 trace: this kernel
@@ -79,11 +73,11 @@ __host__ __device__ inline int r16_xcols(int NG, int k, int dil) {
 __host__ __device__ inline int r16_lds_bytes(int C, int k, int dil) {
   const int xp = C + 8, gp = C / 2 + 8, NG = r16_ng(C);
   const int xsz = r16_xcols(NG, k, dil) * xp, gsz = (NG + 16) * gp;
-  return 2 * (R16_ALIAS ? (xsz > gsz ? xsz : gsz) : xsz + gsz) + 4 * 2 * C + 64;
+  return 2 * (xsz > gsz ? xsz : gsz) + 4 * 2 * C + 64;
 }
 
 template <int C, typename T, bool MEAN>
-__global__ __launch_bounds__(256, (MEAN || !R16_ALIAS) ? 2 : 3) void resblock16_kernel(
+__global__ __launch_bounds__(256, MEAN ? 2 : 3) void resblock16_kernel(
     const R16Group G) {
   constexpr int H = C / 2;
   constexpr int NG = r16_ng(C);
@@ -141,7 +135,7 @@ __global__ __launch_bounds__(256, (MEAN || !R16_ALIAS) ? 2 : 3) void resblock16_
   const int p1 = (k - 1) * dil / 2;
   const int p2 = (k - 1) / 2;
   const int xcols = r16_xcols(NG, k, dil);
-  T* const gs = R16_ALIAS ? xs : xs + xcols * XP;              // [NG + 16][GP]
+  T* const gs = xs;  // [NG + 16][GP], over the dead c1 window
   if (mem > 0) __syncthreads();  // the previous member's reads of LDS are done
 
   // row constants: c1 bias + cond (gate-interleaved order), c2 bias
@@ -256,7 +250,7 @@ __global__ __launch_bounds__(256, (MEAN || !R16_ALIAS) ? 2 : 3) void resblock16_
     // A fragments PF - 1 steps ahead in a register ring (slot = step % PF):
     // one step of TM * TN MFMAs does not cover an L2 round trip.  C5 trace:
     // this kernel family 4.94 -> 4.84 ms per step (profiles/r05_r16pf_*)
-    constexpr int PF = R16_PF;
+    constexpr int PF = 4;
     static_assert(PF == 2 || PF == 4, "ring parity");
     t8 ar[PF][TM], bb[2][TN];
 #pragma unroll
@@ -287,7 +281,7 @@ __global__ __launch_bounds__(256, (MEAN || !R16_ALIAS) ? 2 : 3) void resblock16_
 
   // ---------------- phase 1: c1 over NG columns from n0 - p2 ---------------
   gemm(reinterpret_cast<const T*>(p.w1), p.m_pad1, S1 * k, xs, XP, wn + xsh, dil);
-  if (R16_ALIAS) __syncthreads();  // every wave's window reads are done: G overlays it
+  __syncthreads();  // every wave's window reads are done: G overlays it
 
   // gate epilogue -> G (zero outside [0, L)); the 16 columns past NG that
   // phase 2's discarded columns read are zeroed too

@@ -150,6 +150,11 @@ def _wav_header(fn: str):
                         sr = struct.unpack(en + "I", fmt[4:8])[0]
                         bits = struct.unpack(en + "H", fmt[14:16])[0]
                     elif cid == b"data" and sr is not None and bits:
+                        # a truncated file, or a streamed one with a
+                        # placeholder size (0 / 0xFFFFFFFF): what is there
+                        left = os.path.getsize(fn) - f.tell()
+                        if size == 0 or size > left:
+                            size = left
                         return int(sr), int(size // ((bits + 7) // 8))
                     else:
                         f.seek(size + (size & 1), 1)
@@ -185,12 +190,17 @@ def build_spec_cache(filepaths_sid, hparams, device="cuda", overwrite=False, max
     for _n, items in sorted(todo.items()):
         for i in range(0, len(items), max_batch):
             chunk = items[i:i + max_batch]
-            wavs = torch.stack([load_wav_to_torch(w)[0] for _, w in chunk])
-            spec = _spectrogram(wavs, hp, device)
-            del wavs
-            for (fn, _), s in zip(chunk, spec):
-                torch.save(s.clone(), fn)
-                written += 1
+            loaded = [(fn, load_wav_to_torch(w)[0]) for fn, w in chunk]
+            # (a header that disagrees with the samples read: its own batch)
+            by_len: dict = {}
+            for fn, w in loaded:
+                by_len.setdefault(w.numel(), []).append((fn, w))
+            del loaded
+            for group in by_len.values():
+                spec = _spectrogram(torch.stack([w for _, w in group]), hp, device)
+                for (fn, _), s in zip(group, spec):
+                    torch.save(s.clone(), fn)
+                    written += 1
     return written
 
 

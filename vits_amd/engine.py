@@ -125,11 +125,11 @@ def _conv_eff(conv: torch.nn.Module):
 # ---------------------------------------------------------------------------
 # Generator (HiFi-GAN style decoder with gated ResBlock2)
 # ---------------------------------------------------------------------------
-# grouped launches of the ResBlock2 branches (VITS_GROUP_BRANCHES=0: one
-# launch per conv, for A/B timing)
+# grouped launches of the ResBlock2 branches (False: one launch per conv,
+# for A/B timing in tools/)
 _GROUP_BRANCHES = True
-# fused ResBlock2 pairs on the 32/64-channel stages (VITS_FUSED_PAIRS=0: the
-# two-conv path, for A/B timing and the parity test of both)
+# fused ResBlock2 pairs on the 32/64-channel stages (False: the two-conv
+# path, for A/B timing and the parity test of both)
 _FUSED_PAIRS = True
 # 16-bit models: the last pairs of a stage's branches as one branch-mean
 # launch (vits_resblock_pair16_mean_forward); 0 = one accumulating launch each.
@@ -143,7 +143,7 @@ MEAN_PAIRS16 = True
 # model 40.9 -> 39.0 dB (fp16: 56.2 dB).  The convs there are epilogue /
 # issue-bound rather than HBM-bound, so most of the gain is the global-memory
 # weight path these groups can take (conv1d.hip ga16, io16 = 2).
-# VITS_ACT16=0: fp32 activations (the 16-bit MFMA on fp32 I/O), for A/B.
+# False: fp32 activations (the 16-bit MFMA on fp32 I/O), for A/B.
 ACT16 = True
 
 

@@ -492,8 +492,9 @@ class SynthesizerTrn(nn.Module):
         np.random.randint(numel - C * y_len), drawn on the device from
         ``noise_start`` = int32 [B, ops.ED_DRAWS] raw MT19937 words
         (ops.numpy_draw_pool); the returned y_len is then int32 [2, B]:
-        (y_len, generator words consumed or -1 when the slice does not
-        fit).  ``x_lengths`` (int32 [B]): padded text, encoded
+        (y_len, generator words consumed; -1 when the slice does not
+        fit, -2 when every word of the pool was rejected: the caller
+        advances numpy's generator past the pool and runs again).  ``x_lengths`` (int32 [B]): padded text, encoded
         as TextEncoder.infer of each unpadded utterance (every layer masked,
         engine.TextEncoderPlan pad_exact); None: the exact-length infer_p1
         path (B = 1).  Returns (wav [B, 1, t_y * hop], y_len int32 [B]);

@@ -235,7 +235,7 @@ def _pick_tile_f32p(m: int, k: int) -> int:
 # channels per K-chunk of the pre-split kernel: 32 (two slabs, half the
 # chunk barriers) when the window of a 32-channel chunk fits the staging
 # budget (conv1d_impl.h XTile<BN, true, true>: 6144 / 10240 elements for 128
-# / 256 columns), else 16; VITS_F32P_KC=16 forces single slabs
+# / 256 columns), else 16; F32P_MAX_KC = 16 forces single slabs
 F32P_MAX_KC = 32
 
 
@@ -254,7 +254,7 @@ def _kc_f32p(cin_pad: int, k: int, dil: int, tile: int) -> int:
     return 16
 
 
-# pre-split weights for split fp32 (VITS_SPLIT_W=0: the F32S kernel, which
+# pre-split weights for split fp32 (False: the F32S kernel, which
 # splits the fp32 weight slabs per fragment in registers)
 SPLIT_W = True
 
@@ -700,8 +700,8 @@ def resblock_pair_desc(c1: PackedConv, c2: PackedConv, x: torch.Tensor, y: torch
     return d
 
 
-# fused pairs of 16-bit models (csrc/resblock16.hip): VITS_FUSED_PAIRS16=0
-# keeps their two-conv path
+# fused pairs of 16-bit models (csrc/resblock16.hip): False keeps their
+# two-conv path
 FUSED_PAIRS16 = True
 # largest k fused on the 256-channel stage (resblock_f32p.hip's 16-bit mode;
 # 0 = none, the two-conv path)

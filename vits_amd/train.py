@@ -56,36 +56,68 @@ def build_models(hps, device, variant: str = "stft"):
     return net_g, net_d
 
 
-# G's gradient buckets for the overlapped all-reduce, by parameter-name
-# prefix, in the order the backward finishes them: the decoder's gradients
-# are final first (its backward runs first, and its weight-norm group's
-# backward fires as soon as its last conv's weight gradient is in), then the
-# flow's, the posterior encoder's, and the rest (text encoder, duration
-# predictor, embeddings) last
-G_BUCKETS = ("dec.", "flow.", "enc_q.", "")
+def _layer_prefixes(stem: str, names, idx):
+    return tuple(f"{stem}{n}.{i}." for n in names for i in idx)
+
+
+# G's gradient buckets for the overlapped all-reduce: each is a tuple of
+# parameter-name prefixes (a parameter joins the first bucket with a matching
+# prefix; "" matches all).  Ordered as the backward finishes them, and each at
+# most ~50 MB of fp32 gradients (base.json sizes in the comments): the
+# decoder's late stages first (their weight-norm group's backward fires as
+# soon as their last conv's weight gradient is in), then its first stage, the
+# flow's couplings (reverse order of the forward), the posterior encoder's
+# upper and lower WN layers, the text encoder's upper and lower blocks, and
+# the rest (speaker embedding, duration predictor).  Every bucket is also one
+# weight-norm group (wnorm.WeightNormCache), so its gradients are final
+# together.
+G_BUCKETS = (
+    ("dec.ups.1.", "dec.ups.2.", "dec.ups.3.", "dec.conv_post.")
+    + tuple(f"dec.resblocks.{i}." for i in range(3, 12)),                  # 18 MB
+    ("dec.",),                                                               # 45 MB
+    ("flow.flows.6.", "flow.flows.4."),                                      # 42 MB
+    ("flow.",),                                                              # 42 MB
+    _layer_prefixes("enc_q.enc.", ("in_layers", "res_skip_layers"), range(8, 16))
+    + ("enc_q.proj.",),                                                      # 25 MB
+    ("enc_q.",),                                                             # 26 MB
+    _layer_prefixes("enc_p.encoder.", ("attn_layers", "norm_layers_1", "ffn_layers",
+                                       "norm_layers_2"), range(3, 6)),       # 39 MB
+    ("enc_p.",),                                                             # 41 MB
+    ("",),                                                                   # 13 MB
+)
+
+
+def _bucket_of(name: str, buckets) -> int:
+    return next(i for i, pres in enumerate(buckets) if any(name.startswith(p) for p in pres))
 
 
 class _GradBuckets:
     """Bucketed, overlapped gradient all-reduce for one network (the
     graph-capturable counterpart of DDP's reducer, train_stft.py:108-110):
-    each parameter's post-accumulate-grad hook counts its bucket down, and a
-    bucket whose gradients are all final is averaged over the ranks at once
-    - on the GPU on a side stream (forked from the backward's stream by an
-    event: copy into one flat buffer, one RCCL all-reduce over xGMI, scale,
-    copy back) while the backward of the earlier layers continues; on CPU
-    (gloo) synchronously.  finish() launches any bucket still waiting (a
-    parameter without a gradient this step) and joins the side stream."""
+    each parameter's post-accumulate-grad hook counts its bucket down; a
+    bucket whose gradients are all final is averaged over the ranks - on the
+    GPU on a side stream (forked from the backward's stream by an event:
+    copy into one flat buffer, one RCCL all-reduce over xGMI, scale, copy
+    back) while the backward of the earlier layers continues; on CPU (gloo)
+    synchronously.
 
-    def __init__(self, net, prefixes, device):
+    Collectives must pair up across ranks, so buckets are launched strictly
+    by index (as DDP's reducer does): a bucket that completes early waits
+    until every lower-indexed bucket has been launched.  finish() launches
+    whatever is still waiting, in order, and joins the side stream.  Every
+    bucket always holds ALL its parameters: one without a gradient this step
+    (unused on this rank - an error under the reference's DDP) contributes
+    zeros, so every rank's flat layout is the same."""
+
+    def __init__(self, net, buckets, device):
         self.device = device
         named = [(n, p) for n, p in net.named_parameters() if p.requires_grad]
-        self.buckets = [[] for _ in prefixes]
+        self.buckets = [[] for _ in buckets]
         for n, p in named:
-            i = next(i for i, pre in enumerate(prefixes) if n.startswith(pre))
-            self.buckets[i].append(p)
+            self.buckets[_bucket_of(n, buckets)].append(p)
         self.buckets = [b for b in self.buckets if b]
         self.comm = torch.cuda.Stream(device) if device.type == "cuda" else None
-        self._flat = {}
+        self._flat = [None] * len(self.buckets)
         self._left = None
         self._hooks = []
         for bi, ps in enumerate(self.buckets):
@@ -95,32 +127,31 @@ class _GradBuckets:
 
     def begin(self):
         self._left = [len(b) for b in self.buckets]
-        self._done = [False] * len(self.buckets)
+        self._next = 0  # lowest bucket index not yet launched
 
     def _arrived(self, bi):
         if self._left is None:  # (a backward outside step(): no all-reduce)
             return
         self._left[bi] -= 1
-        if self._left[bi] == 0:
-            self._launch(bi)
+        # launch, in index order, every bucket whose gradients are complete
+        while self._next < len(self.buckets) and self._left[self._next] == 0:
+            self._launch(self._next)
+            self._next += 1
 
     def _launch(self, bi):
-        self._done[bi] = True
-        ps = [p for p in self.buckets[bi] if p.grad is not None]
-        if not ps:
-            return
-        key = tuple(id(p) for p in ps)
-        ent = self._flat.get((bi, key))
-        if ent is None:
+        ps = self.buckets[bi]
+        for p in ps:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        if self._flat[bi] is None:
             flat = torch.empty(sum(p.numel() for p in ps), device=ps[0].device,
                                dtype=torch.float32)
             views, o = [], 0
             for p in ps:
                 views.append(flat[o:o + p.numel()].view_as(p))
                 o += p.numel()
-            ent = (flat, views)
-            self._flat[(bi, key)] = ent
-        flat, views = ent
+            self._flat[bi] = (flat, views)
+        flat, views = self._flat[bi]
         grads = [p.grad for p in ps]
         if self.comm is None:
             torch._foreach_copy_(views, grads)
@@ -137,9 +168,9 @@ class _GradBuckets:
             torch._foreach_copy_(grads, views)
 
     def finish(self):
-        for bi, done in enumerate(self._done):
-            if not done:
-                self._launch(bi)
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
         self._left = None
         if self.comm is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm)
@@ -220,7 +251,7 @@ class TrainStep:
         self.net_g, self.net_d = net_g, net_d
         # every weight-normed generator layer in one launch each way (GPU)
         self._wn_g = (WeightNormCache(net_g.module if isinstance(net_g, DDP) else net_g,
-                                      G_BUCKETS if self._gbuckets is not None else ("",))
+                                      G_BUCKETS if self._gbuckets is not None else (("",),))
                       if device.type == "cuda" else None)
         fp16 = bool(hps.train.fp16_run) and device.type == "cuda"
         # the autocast weight-cast cache must be off under graph capture (cached

@@ -97,7 +97,7 @@ def _train_kc(cin_pad: int, k: int, dil: int, tile: int, io16: bool) -> int:
     return 16
 
 
-# per-call weight packs by call site (tools/pack_census.py; VITS_PACK_TRACE=1)
+# per-call weight packs by call site (tools/pack_census.py sets it)
 PACK_TRACE = None  # tools/pack_census.py sets a collections.Counter()
 
 
@@ -986,7 +986,7 @@ def conv_transpose1d(module: nn.Module, x: torch.Tensor, in_slope: float = 1.0) 
 # ---------------------------------------------------------------------------
 # in_layer / convs1 convs whose output only feeds the tanh * sigmoid gate run
 # the GATE epilogue (gate-interleaved weight rows) and write the
-# pre-activation for the gate's backward in the same launch; VITS_GATE_FUSED=0
+# pre-activation for the gate's backward in the same launch; False (tests)
 # keeps the separate conv + GateHip16 kernels
 GATE_FUSED = True
 

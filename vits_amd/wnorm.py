@@ -114,11 +114,14 @@ class WeightNormCache:
     computed for all of them by one ``vits_weight_norm_forward`` launch."""
 
     def __init__(self, root: torch.nn.Module, groups=("",)):
-        """groups: module-name prefixes; each group's weights come from one
-        launch and go back in one (its backward runs as soon as that group's
-        last weight gradient is in: the decoder's long before the text
-        encoder's, so its gradients can be all-reduced while the rest of the
-        backward runs - train._GradBuckets)."""
+        """groups: one tuple of module-name prefixes per group (a plain
+        string is a one-prefix group; a module joins the first group with a
+        matching prefix); each group's weights come from one launch and go
+        back in one (its backward runs as soon as that group's last weight
+        gradient is in: the decoder's long before the text encoder's, so its
+        gradients can be all-reduced while the rest of the backward runs -
+        train._GradBuckets)."""
+        groups = [(g,) if isinstance(g, str) else tuple(g) for g in groups]
         self.mods = []
         self.groups = [[] for _ in groups]
         for name, m in root.named_modules():
@@ -129,7 +132,8 @@ class WeightNormCache:
             if g.dtype == v.dtype == torch.float32 and v.is_cuda and v.is_contiguous() \
                     and g.is_contiguous() and g.numel() == v.shape[0]:
                 self.mods.append((m, h.name))
-                gi = next(i for i, pre in enumerate(groups) if (name + ".").startswith(pre))
+                gi = next(i for i, pres in enumerate(groups)
+                          if any((name + ".").startswith(pre) for pre in pres))
                 self.groups[gi].append((m, h.name))
         self.groups = [grp for grp in self.groups if grp]
 
