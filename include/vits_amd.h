@@ -452,6 +452,30 @@ int vits_gate_backward_io16(const void* dy, int64_t dy_bstride, int32_t dy_cstri
                             float* dg, int batch, int half_channels, int t_len, int wdtype,
                             void* stream);
 
+/* Up to 4 independent vits_gate_backward_io16 jobs of one batch and length */
+/* as ONE launch (the three ResBlock2 branches of a Generator stage,         */
+/* modules.py:253-255 under train_stft.py:165's autocast); dg of job i at    */
+/* dg[b * dg_bstride + c] (a column slice of the stage's cond gradient).     */
+typedef struct vits_gate_bwd_job {
+  const void* dy;
+  int64_t dy_bstride;
+  int64_t dy_cstride;
+  const void* x;
+  int64_t x_bstride;
+  int64_t x_cstride;
+  const void* g;         /* 16-bit cond [B][g_bstride], or NULL */
+  int64_t g_bstride;
+  void* dx;
+  int64_t dx_bstride;
+  int64_t dx_cstride;
+  float* dg;             /* fp32, or NULL */
+  int64_t dg_bstride;
+  int32_t half_channels;
+  int32_t reserved;
+} vits_gate_bwd_job;
+int vits_gate_backward_io16_multi(const vits_gate_bwd_job* jobs, int n, int batch, int t_len,
+                                  int wdtype, void* stream);
+
 /* ---------------------------------------------------------------------- */
 /* One ResBlock2 dilation pair of the Generator as ONE kernel              */
 /* (modules.py:250-260, fp32):                                             */

@@ -40,21 +40,22 @@ def test_struct_layout_matches_header():
     import subprocess
     import tempfile
 
-    from vits_amd._lib import (WNORM_MAX, SNORM_MAX, ConvDesc, ConvOut, Pack16Layer,
+    from vits_amd._lib import (WNORM_MAX, SNORM_MAX, ConvDesc, ConvOut, GateBwdJob, Pack16Layer,
                                ResblockPairDesc, SnormLayer, StftJob, WnormLayer)
 
     probe = r'''
 #include <stdio.h>
 #include <stddef.h>
 #include "vits_amd.h"
-int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc),
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vits_conv1d_desc),
  sizeof(vits_conv_out), offsetof(vits_conv1d_desc, out0), offsetof(vits_conv1d_desc, lengths),
  offsetof(vits_conv1d_desc, wdtype), sizeof(vits_stft_job), offsetof(vits_stft_job, eps),
  sizeof(vits_resblock_pair_desc), offsetof(vits_resblock_pair_desc, w2),
  offsetof(vits_resblock_pair_desc, post_div), sizeof(vits_wnorm_layer),
  sizeof(vits_snorm_layer), offsetof(vits_snorm_layer, eps), VITS_WNORM_MAX, VITS_SNORM_MAX,
  sizeof(vits_pack16_layer), offsetof(vits_pack16_layer, img_t), offsetof(vits_pack16_layer, cin_pad_t),
- offsetof(vits_conv1d_desc, gmask_slope), offsetof(vits_conv1d_desc, len_skip));
+ offsetof(vits_conv1d_desc, gmask_slope), offsetof(vits_conv1d_desc, len_skip),
+ sizeof(vits_gate_bwd_job), offsetof(vits_gate_bwd_job, half_channels));
  return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -83,6 +84,8 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %zu
     assert int(out[17]) == Pack16Layer.cin_pad_t.offset
     assert int(out[18]) == ConvDesc.gmask_slope.offset
     assert int(out[19]) == ConvDesc.len_skip.offset
+    assert int(out[20]) == ctypes.sizeof(GateBwdJob)
+    assert int(out[21]) == GateBwdJob.half_channels.offset
 
 
 def test_dispatch_counters_host_side():

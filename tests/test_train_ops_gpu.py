@@ -636,3 +636,65 @@ def test_qkv_cat_matches_three_convs(device, monkeypatch):
     for i, (u, v) in enumerate(zip(a, b)):
         err = (u.float() - v.float()).abs().max().item() / u.float().abs().max().item()
         assert err <= 2e-3, (i, err)
+
+
+def test_resblock_stage_grouped_matches_per_branch(device, monkeypatch):
+    """train_ops.ResblockStage16 (a Generator stage's three ResBlock2 branches
+    as grouped launches, their gate backwards as one multi-job launch) against
+    the per-branch ResBlock2 path on the base config's decoder under fp16
+    autocast with the prepacked images, 8 frames x 2 utterances (every stage:
+    256 / 128 / 64 / 32 channels; T = 64 .. 1536).  Forward: bit-identical
+    (same kernels and k-order, only the launch grouping differs), with 6
+    forward conv launches per stage instead of 18.  Gradients: the grouped
+    input gradient rounds `residual + conv` to fp16 once where autograd rounds
+    the conv and then the add, so both are measured against the same step in
+    fp32 (autocast off: the fp32 HIP training kernels) and the grouped path
+    must be as close to it as the per-branch path (relative L2 within 1.25x
+    + 1e-4 per tensor) and within 1e-2 relative L2 of the per-branch path."""
+    from common import base_model
+    from vits_amd import _lib
+    from vits_amd.wnorm import WeightNormCache
+
+    torch.manual_seed(11)
+    m = base_model(device)
+    dec = m.dec.train()
+    z = torch.randn(2, 192, 8, device=device)
+    g = torch.randn(2, 1024, device=device) * 0.5
+    cache = WeightNormCache(dec)
+
+    def run(grouped, fp16=True):
+        monkeypatch.setattr(train_ops, "STAGE_GROUPED", grouped)
+        for p in dec.parameters():
+            p.grad = None
+        zi = z.clone().requires_grad_(True)
+        gi = g.clone().requires_grad_(True)
+        _lib.dispatch_counts_reset()
+        with torch.autocast("cuda", dtype=torch.float16, enabled=fp16), cache.active(), \
+                train_ops.prepacked(dec):
+            y = dec(zi, gi)
+        torch.cuda.synchronize()
+        nconv = _lib.dispatch_counts()["conv_16"]
+        (y.float() * torch.linspace(-1, 1, y.shape[-1], device=device)).sum().backward()
+        grads = {n: p.grad.detach().double().clone() for n, p in dec.named_parameters()
+                 if p.grad is not None}
+        grads["dz"], grads["dg"] = zi.grad.double(), gi.grad.double()
+        return y.detach().clone(), grads, nconv
+
+    ya, ga, na = run(False)
+    yb, gb, nb = run(True)
+    _, gr, _ = run(False, fp16=False)
+    assert torch.equal(ya, yb), (ya.float() - yb.float()).abs().max().item()
+    assert nb == na - 4 * 12, (na, nb)  # 4 stages: 6 grouped launches instead of 18
+    assert set(ga) == set(gb) == set(gr)
+
+    def rl2(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+    worst = []
+    for n in ga:
+        if gr[n].norm() == 0:
+            continue
+        ea, eb = rl2(ga[n], gr[n]), rl2(gb[n], gr[n])
+        worst.append((eb - ea, n, ea, eb))
+        assert eb <= 1.25 * ea + 1e-4 and rl2(gb[n], ga[n]) < 1e-2, (n, ea, eb)
+    print("largest grouped-minus-per-branch error vs fp32:", sorted(worst)[-3:])

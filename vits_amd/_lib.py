@@ -162,6 +162,27 @@ class ConvWgradDesc(C.Structure):
     ]
 
 
+class GateBwdJob(C.Structure):
+    """vits_gate_bwd_job (one job of vits_gate_backward_io16_multi)."""
+    _fields_ = [
+        ("dy", C.c_void_p),
+        ("dy_bstride", C.c_int64),
+        ("dy_cstride", C.c_int64),
+        ("x", C.c_void_p),
+        ("x_bstride", C.c_int64),
+        ("x_cstride", C.c_int64),
+        ("g", C.c_void_p),
+        ("g_bstride", C.c_int64),
+        ("dx", C.c_void_p),
+        ("dx_bstride", C.c_int64),
+        ("dx_cstride", C.c_int64),
+        ("dg", C.c_void_p),
+        ("dg_bstride", C.c_int64),
+        ("half_channels", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
 RADAM_MAX = 96
 
 
@@ -343,6 +364,8 @@ _SIGS = {
          C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
          C.c_void_p],
     ),
+    "vits_gate_backward_io16_multi": (
+        C.c_int, [C.POINTER(GateBwdJob), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "vits_radam_step": (
         C.c_int,
         [C.POINTER(RadamTensor), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,

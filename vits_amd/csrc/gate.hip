@@ -39,18 +39,17 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const E* __restrict__ x, 
 // V4: rows 4-element aligned (T % 4 == 0, strides and bases aligned): one
 // 4-element load / store per row and thread - the element-wise map issued a
 // 2-byte access per lane (half-width transactions) and left most of a
-// T = 500 row's threads idle after two iterations
-template <typename E, bool V4 = false>
-__global__ __launch_bounds__(256) void gate_bwd_kernel(const E* __restrict__ dy, int64_t dy_bs,
-                                                      int dy_cs, const E* __restrict__ x,
-                                                      int64_t x_bs, int x_cs,
-                                                      const E* __restrict__ g, int64_t g_bs,
-                                                      E* __restrict__ dx, int64_t dx_bs,
-                                                      int dx_cs, float* __restrict__ dg, int H,
-                                                      int T) {
+// T = 500 row's threads idle after two iterations.  One workgroup = one
+// (b, p) row pair; dg[b * dg_bs + p] / [... + H + p] (dg_bs = 2H: the
+// [B][2H] cond gradient; larger: a column slice of a wider buffer).
+template <typename E, bool V4>
+__device__ __forceinline__ void gate_bwd_rows(const E* __restrict__ dy, int64_t dy_bs, int dy_cs,
+                                              const E* __restrict__ x, int64_t x_bs, int x_cs,
+                                              const E* __restrict__ g, int64_t g_bs,
+                                              E* __restrict__ dx, int64_t dx_bs, int dx_cs,
+                                              float* __restrict__ dg, int64_t dg_bs, int H, int T,
+                                              int p, int b) {
   __shared__ float red[2][4];
-  const int p = blockIdx.x;
-  const int b = blockIdx.y;
   const E* xa = x + (int64_t)b * x_bs + (int64_t)p * x_cs;
   const E* xb = xa + (int64_t)H * x_cs;
   const E* dyr = dy + (int64_t)b * dy_bs + (int64_t)p * dy_cs;
@@ -103,10 +102,42 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const E* __restrict__ dy,
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      dg[(int64_t)b * 2 * H + p] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-      dg[(int64_t)b * 2 * H + H + p] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      dg[(int64_t)b * dg_bs + p] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      dg[(int64_t)b * dg_bs + H + p] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     }
   }
+}
+
+template <typename E, bool V4 = false>
+__global__ __launch_bounds__(256) void gate_bwd_kernel(const E* __restrict__ dy, int64_t dy_bs,
+                                                      int dy_cs, const E* __restrict__ x,
+                                                      int64_t x_bs, int x_cs,
+                                                      const E* __restrict__ g, int64_t g_bs,
+                                                      E* __restrict__ dx, int64_t dx_bs,
+                                                      int dx_cs, float* __restrict__ dg, int H,
+                                                      int T) {
+  gate_bwd_rows<E, V4>(dy, dy_bs, dy_cs, x, x_bs, x_cs, g, g_bs, dx, dx_bs, dx_cs, dg, 2 * H, H,
+                       T, blockIdx.x, blockIdx.y);
+}
+
+// up to GATE_JOBS independent gate backwards of one batch / length (the
+// three ResBlock2 branches of a Generator stage) as one grid: blockIdx.z
+// selects the job
+constexpr int GATE_JOBS = 4;
+struct GateJobs {
+  vits_gate_bwd_job j[GATE_JOBS];
+  int n;
+};
+
+template <typename E, bool V4>
+__global__ __launch_bounds__(256) void gate_bwd_multi_kernel(const GateJobs J, int T) {
+  const vits_gate_bwd_job& q = J.j[blockIdx.z];
+  if ((int)blockIdx.x >= q.half_channels) return;
+  gate_bwd_rows<E, V4>(static_cast<const E*>(q.dy), q.dy_bstride, q.dy_cstride,
+                       static_cast<const E*>(q.x), q.x_bstride, q.x_cstride,
+                       static_cast<const E*>(q.g), q.g_bstride, static_cast<E*>(q.dx),
+                       q.dx_bstride, q.dx_cstride, q.dg, q.dg_bstride, q.half_channels, T,
+                       blockIdx.x, blockIdx.y);
 }
 
 }  // namespace
@@ -190,5 +221,41 @@ extern "C" int vits_gate_backward_io16(const void* dy, int64_t dy_bstride, int32
   else
     return VITS_E_ARG;
 #undef VITS_GATE_BWD
+  return count_ok(vits_launch_status(), VITS_CNT_GATE_16);
+}
+
+extern "C" int vits_gate_backward_io16_multi(const vits_gate_bwd_job* jobs, int n, int batch,
+                                             int t_len, int wdtype, void* stream) {
+  VITS_CHECK_ARG(jobs && n > 0 && n <= GATE_JOBS && batch > 0 && t_len > 0);
+  VITS_CHECK_SHAPE(batch <= 65535);
+  GateJobs J;
+  J.n = n;
+  int hmax = 0;
+  bool v4 = (t_len & 3) == 0;
+  for (int i = 0; i < n; ++i) {
+    const vits_gate_bwd_job& q = jobs[i];
+    VITS_CHECK_ARG(q.dy && q.x && q.dx && q.half_channels > 0);
+    if (q.dg) VITS_CHECK_ARG(q.dg_bstride >= 2 * (int64_t)q.half_channels);
+    J.j[i] = q;
+    hmax = q.half_channels > hmax ? q.half_channels : hmax;
+    v4 = v4 && ((q.dy_bstride | q.dy_cstride | q.x_bstride | q.x_cstride | q.dx_bstride |
+                 q.dx_cstride | (int64_t)q.half_channels) & 3) == 0 &&
+         ((reinterpret_cast<uintptr_t>(q.dy) | reinterpret_cast<uintptr_t>(q.x) |
+           reinterpret_cast<uintptr_t>(q.dx)) & 7) == 0;
+  }
+  const dim3 grid(hmax, batch, n);
+  hipStream_t s = as_stream(stream);
+#define VITS_GATE_BWDM(E)                                                                          \
+  if (v4)                                                                                          \
+    hipLaunchKernelGGL((gate_bwd_multi_kernel<E, true>), grid, dim3(256), 0, s, J, t_len);        \
+  else                                                                                             \
+    hipLaunchKernelGGL((gate_bwd_multi_kernel<E, false>), grid, dim3(256), 0, s, J, t_len)
+  if (wdtype == VITS_WDT_F16)
+    VITS_GATE_BWDM(_Float16);
+  else if (wdtype == VITS_WDT_BF16)
+    VITS_GATE_BWDM(__bf16);
+  else
+    return VITS_E_ARG;
+#undef VITS_GATE_BWDM
   return count_ok(vits_launch_status(), VITS_CNT_GATE_16);
 }

@@ -248,15 +248,22 @@ class Generator(nn.Module):
             # inference: HIP plan only (raises off-GPU; there is no CPU path)
             return engine.generator_forward(self, x, g)
         x = train_ops.conv1d(self.conv_pre, x)
-        conds = self._resblock_conds(g)
+        conds, y16, y32 = self._resblock_conds(g)
+        col0 = 0
         for i in range(self.num_upsamples):
             # polyphase on the HIP training conv under autocast (torch otherwise)
             x = train_ops.conv_transpose1d(self.ups[i], x, in_slope=modules.LRELU_SLOPE)
-            xs = 0
-            for j in range(self.num_kernels):
-                rb = i * self.num_kernels + j
-                xs = xs + self.resblocks[rb](x, g=g, conds=None if conds is None else conds[rb])
-            x = xs / self.num_kernels
+            rbs = self.resblocks[i * self.num_kernels:(i + 1) * self.num_kernels]
+            # the stage's branches as grouped launches (fp16 autocast on the GPU)
+            xs = train_ops.resblock_stage(x, rbs, y16, y32, col0)
+            if xs is None:
+                xs = 0
+                for j in range(self.num_kernels):
+                    rb = i * self.num_kernels + j
+                    xs = xs + self.resblocks[rb](x, g=g, conds=None if conds is None else conds[rb])
+                xs = xs / self.num_kernels
+            x = xs
+            col0 += sum(cs.out_features for rb in rbs for cs in rb.conds)
         x = train_ops.conv1d(self.conv_post, x, in_slope=0.01)  # F.leaky_relu default slope
         return torch.tanh(x)
 
@@ -265,12 +272,14 @@ class Generator(nn.Module):
         dilation pair, 36 at the base config, all applied to the same g) as
         ONE GEMM over the concatenated weights, split back per resblock:
         the same products, one launch instead of 36 (each with its own
-        autocast casts and backward GEMMs).  None without a speaker vector."""
+        autocast casts and backward GEMMs).  Returns (per-resblock conds,
+        the GEMM's output y, its fp32 copy y32 or None), or (None, None,
+        None) without a speaker vector."""
         if g is None or not g.is_cuda:
-            return None
+            return None, None, None
         mods = [cs for rb in self.resblocks for cs in rb.conds]
         if not all(isinstance(m, nn.Linear) and m.bias is not None for m in mods):
-            return None
+            return None, None, None
         ws = [train_ops.module_weight(m) for m in mods]
         y = F.linear(g, torch.cat(ws, 0), torch.cat([m.bias for m in mods]))
         sizes = [w.shape[0] for w in ws]
@@ -279,7 +288,7 @@ class Generator(nn.Module):
         if y32 is not None:
             parts = list(zip(parts, torch.split(y32, sizes, dim=1)))
         k = len(self.resblocks[0].conds)
-        return [parts[i * k:(i + 1) * k] for i in range(len(self.resblocks))]
+        return [parts[i * k:(i + 1) * k] for i in range(len(self.resblocks))], y, y32
 
     def infer(self, x, g):
         return self.forward(x, g)

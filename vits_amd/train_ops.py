@@ -51,6 +51,7 @@ from ._lib import (EPI_GATE, EPI_STORE, TILE_32x256, TILE_64x128, TILE_64x256, T
                    WDT_BF16, WDT_F16, WDT_F32, ConvWgradDesc, check)
 from . import engine
 from .ops import (PackedConv, _pick_tile_bf16, _stream_ptr, cached_weight, conv1d_launch,
+                  conv1d_launch_seq,
                   make_desc, make_out,
                   pack_conv, to_lowp, weight_norm_effective)
 
@@ -1129,3 +1130,189 @@ def conv1d_gate(module: nn.Module, x: torch.Tensor, g, in_slope: float = 1.0, g1
         g16 = None
     return ConvGateHip16.apply(x if x.dtype == t16 else x.to(t16), w, module.bias, g,
                                module.dilation[0], module.padding[0], in_slope, wdt, pre, g16)
+
+
+# ---------------------------------------------------------------------------
+# a Generator stage's three ResBlock2 branches as grouped launches
+# (models.py:311-313, modules.py:250-260) under fp16 autocast
+# ---------------------------------------------------------------------------
+# The stage's branches (k = 3, 7, 11) read the same input and are independent
+# until their mean, so pair p of every branch runs as ONE grouped launch
+# (vits_conv1d_forward_groups, blockIdx.z = branch x utterance) each way:
+# forward c1 + gate and c2 + residual, backward c2's input gradient, the
+# three gate backwards (vits_gate_backward_io16_multi) and c1's input
+# gradient with the leaky-relu derivative and the residual gradient in its
+# epilogue.  Per stage 6 forward conv launches instead of 18 and 9 backward
+# ones instead of 27, with three times the workgroups of one conv - the
+# 48-frame decoder slices' 256-channel stage alone is 1.2 rounds of the chip.
+# False: the per-branch ResBlock2.forward (Conv1dHip16 / ConvGateHip16).
+STAGE_GROUPED = True
+RB_SLOPE = 0.1  # modules.LRELU_SLOPE (modules.py:251)
+
+
+def _stage_tile(m: int, T: int) -> int:
+    """One tile for all three branches of a grouped launch (their own tile
+    picks differ by k): 32-row layers 32x256, else 64x256 on time rows of
+    whole 256-column tiles, 64x128 otherwise (the 384-frame stage)."""
+    if m <= 32:
+        return TILE_32x256
+    return TILE_64x256 if T % 256 == 0 else TILE_64x128
+
+
+def _img_layer(img, chans: int, rows: int, k: int, dil: int, pad_left: int, epi: int, T: int,
+               wdtype: int, bias=None) -> PackedConv:
+    tile = _stage_tile(rows, T)
+    kc = _train_kc(img.shape[0] * 16, k, dil, tile, True)
+    return PackedConv(img, bias, chans, rows, k, dil, pad_left, epi, tile, kc, out_channels=rows,
+                      wdtype=wdtype)
+
+
+def _gmask_desc(d, gm: torch.Tensor, slope: float):
+    d.gmask, d.gmask_bstride, d.gmask_cstride = gm.data_ptr(), gm.stride(0), gm.stride(1)
+    d.gmask_slope = slope
+    return d
+
+
+class ResblockStage16(torch.autograd.Function):
+    """The three ResBlock2 branches of one Generator stage on fp16
+    activations (x, the gated tensors, pre-activations, outputs and their
+    gradients fp16; W / b fp32 masters, packed by ``prepacked``), returning
+    the branch mean ((x0 + x1) + x2) / 3 as the reference's Generator sums
+    them (models.py:311-313).
+
+    forward(x, cond32, cond16, meta, *params): cond32 / cond16 are the
+    stage's columns of the conditioning Linears' output (fp32 copy for the
+    gate epilogue, 16-bit for the gate backward), meta[j][p] = (k, dil,
+    pad1, pad2, column, (img1, img1_t), (img2, img2_t), wdtype), params =
+    (w1, b1, w2, b2) per (branch j, pair p), branch-major."""
+
+    @staticmethod
+    def forward(ctx, x, cond32, cond16, meta, *params):
+        B, C, T = x.shape
+        H = C // 2
+        dev = x.device
+        wdt = meta[0][0][7]
+        xs = [x, x, x]
+        saved = []
+        for p in range(3):
+            acts = [torch.empty(B, H, T, device=dev, dtype=x.dtype) for _ in range(3)]
+            xins = [torch.empty(B, C, T, device=dev, dtype=x.dtype) for _ in range(3)]
+            ys = [torch.empty(B, C, T, device=dev, dtype=x.dtype) for _ in range(3)]
+            g1, g2 = [], []
+            for j in range(3):
+                k, dil, pad1, pad2, col, im1, im2, _ = meta[j][p]
+                w1, b1, w2, b2 = params[4 * (3 * j + p):4 * (3 * j + p) + 4]
+                l1 = _img_layer(im1[0], C, C, k, dil, pad1, EPI_GATE, T, wdt,
+                                b1.detach().float().contiguous())
+                g1.append(make_desc(l1, xs[j], make_out(acts[j]), out1=make_out(xins[j]),
+                                    in_slope=RB_SLOPE, tin=T, n_out=T, cond=cond32,
+                                    cond_offset=col, io16=True))
+                l2 = _img_layer(im2[0], H, C, k, 1, pad2, EPI_STORE, T, wdt,
+                                b2.detach().float().contiguous())
+                g2.append(make_desc(l2, acts[j], make_out(ys[j], res=xs[j]), tin=T, n_out=T,
+                                    io16=True))
+            conv1d_launch_seq([tuple(g1)], B, dev)
+            conv1d_launch_seq([tuple(g2)], B, dev)
+            saved.append((list(xs), acts, xins))
+            xs = ys
+        out = (xs[0] + xs[1] + xs[2]) / 3
+        ctx.meta = meta
+        ctx.stage = saved
+        ctx.save_for_backward(cond16)
+        ctx.nparams = len(params)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (cond16,) = ctx.saved_tensors
+        meta = ctx.meta
+        x0 = ctx.stage[0][0][0]
+        B, C, T = x0.shape
+        H = C // 2
+        dev = x0.device
+        wdt = meta[0][0][7]
+        lib = _lib.load()
+        G = (g.to(x0.dtype) / 3).contiguous()  # DivBackward of the branch mean
+        Gs = [G, G, G]
+        dparams = [None] * ctx.nparams
+        dcond = torch.empty(B, 9 * C, device=dev, dtype=torch.float32)
+        for p in (2, 1, 0):
+            xs, acts, xins = ctx.stage[p]
+            dacts = [torch.empty(B, H, T, device=dev, dtype=x0.dtype) for _ in range(3)]
+            dxins = [torch.empty(B, C, T, device=dev, dtype=x0.dtype) for _ in range(3)]
+            dxs = [torch.empty(B, C, T, device=dev, dtype=x0.dtype) for _ in range(3)]
+            g2, g1 = [], []
+            jobs = (_lib.GateBwdJob * 3)()
+            for j in range(3):
+                k, dil, pad1, pad2, col, im1, im2, _ = meta[j][p]
+                l2t = _img_layer(im2[1], C, H, k, 1, (k - 1) - pad2, EPI_STORE, T, wdt)
+                g2.append(make_desc(l2t, Gs[j], make_out(dacts[j]), tin=T, n_out=T, io16=True))
+                q = jobs[j]
+                q.dy, q.dy_bstride, q.dy_cstride = dacts[j].data_ptr(), H * T, T
+                q.x, q.x_bstride, q.x_cstride = xins[j].data_ptr(), C * T, T
+                q.g = cond16.data_ptr() + cond16.element_size() * col
+                q.g_bstride = cond16.stride(0)
+                q.dx, q.dx_bstride, q.dx_cstride = dxins[j].data_ptr(), C * T, T
+                q.dg, q.dg_bstride = dcond.data_ptr() + 4 * (3 * j + p) * C, 9 * C
+                q.half_channels = H
+                l1t = _img_layer(im1[1], C, C, k, dil, (k - 1) * dil - pad1, EPI_STORE, T, wdt)
+                g1.append(_gmask_desc(
+                    make_desc(l1t, dxins[j], make_out(dxs[j], res=Gs[j]), tin=T, n_out=T,
+                              io16=True), xs[j], RB_SLOPE))
+            conv1d_launch_seq([tuple(g2)], B, dev)
+            check(lib.vits_gate_backward_io16_multi(jobs, 3, B, T, wdt, _stream_ptr(dev)),
+                  "vits_gate_backward_io16_multi")
+            conv1d_launch_seq([tuple(g1)], B, dev)
+            for j in range(3):
+                k, dil, pad1, pad2 = meta[j][p][:4]
+                i0 = 4 * (3 * j + p)
+                dparams[i0 + 2], dparams[i0 + 3] = wgrad(Gs[j], acts[j], k, 1, pad2, 1.0,
+                                                         wdtype=wdt, split=True)
+                dparams[i0], dparams[i0 + 1] = wgrad(dxins[j], xs[j], k, dil, pad1, RB_SLOPE,
+                                                     wdtype=wdt, split=True)
+            Gs = dxs
+        dx = Gs[0] + Gs[1] + Gs[2]
+        ctx.stage = None
+        return (dx, dcond, None, None, *dparams)
+
+
+def resblock_stage(x: torch.Tensor, resblocks, y16: torch.Tensor, y32: torch.Tensor, col0: int):
+    """mean_j resblocks[j](x) for a Generator stage's three ResBlock2 (their
+    conditioning Linears' outputs are the columns col0 .. of y16 / y32, the
+    Generator's one conditioning GEMM) as ResblockStage16, or None when it
+    does not apply (not the fp16 autocast training step, weights not
+    prepacked, another topology): the caller runs the branches one by one."""
+    wdt = train_wdtype(x)
+    if (not STAGE_GROUPED or wdt is None or not _io16(wdt) or len(resblocks) != 3
+            or x.dim() != 3 or y16 is None or y32 is None):
+        return None
+    t16 = _TORCH_16[wdt]
+    C = x.shape[1]
+    meta, params = [], []
+    col = 0
+    for rb in resblocks:
+        if (len(rb.convs1) != 3 or rb.convs1[0].out_channels != C or rb.convs1[0].in_channels != C
+                or C % 32):
+            return None
+        row = []
+        for c1, c2 in zip(rb.convs1, rb.convs2):
+            w1, w2 = weight_norm_effective(c1), weight_norm_effective(c2)
+            e1, e2 = _PREPACK.get(c1), _PREPACK.get(c2)
+            if (e1 is None or e2 is None or e1[0] is not w1 or e2[0] is not w2 or e1[2] != wdt
+                    or e2[2] != wdt or not e1[3] or e2[3] or c1.bias is None or c2.bias is None
+                    or c1.padding[0] * 2 != (c1.kernel_size[0] - 1) * c1.dilation[0]
+                    or c2.padding[0] * 2 != c2.kernel_size[0] - 1 or c2.dilation[0] != 1):
+                return None
+            row.append((c1.kernel_size[0], c1.dilation[0], c1.padding[0], c2.padding[0], col,
+                        e1[1], e2[1], wdt))
+            params += [w1, c1.bias, w2, c2.bias]
+            col += C
+        meta.append(row)
+    x16 = (x if x.dtype == t16 else x.to(t16)).contiguous()
+    if x16.shape[2] % 4:
+        return None
+    cond32 = y32[:, col0:col0 + col]
+    cond16 = y16[:, col0:col0 + col]
+    if cond16.dtype != t16:
+        return None
+    return ResblockStage16.apply(x16, cond32, cond16, meta, *params)
