@@ -39,6 +39,10 @@ Fixtures (npz, float32 unless noted):
                       gradient statistics and post-step parameter statistics
                       (RAdam for D, AdamW for G as the reference builds them);
                       train_step_config.json the config.
+  train_step_base.npz the same step at configs/base.json widths (Tx 20,
+                      Ty 100); train_step_base_config.json.
+  train_step_adv.npz  the tiny step with c_stft = 0 (adversarial, duration
+                      and KL losses only); train_step_adv_config.json.
   base_c5.npz         one C5 long-form utterance (Tx=500, Ty=2500) through
                       the reference's bf16 model and its fp32 model:
                       waveform windows / statistics, reference SNR
@@ -48,7 +52,7 @@ Fixtures (npz, float32 unless noted):
                       decoder, z statistics; plus SynthesizerTrn.infer at
                       Tx=12 with its noise draw recorded.
 
-Usage: python tests/golden/make_golden.py [mpd|mwsd|train_step|c1 ...]
+Usage: python tests/golden/make_golden.py [mpd|mwsd|train_step|train_step_base|train_step_adv|c1 ...]
 """
 from __future__ import annotations
 
@@ -362,12 +366,29 @@ TRAIN_STEP = dict(seg_frames=16, B=2, Tx=10, Ty=40, x_lengths=[10, 8], y_lengths
                   align_noise_decay=1e-6)
 
 
-def train_step_inputs():
-    c = TRAIN_STEP
+# the same step at configs/base.json widths (B=2, Tx 20, Ty 100): every HIP
+# training kernel at the benchmarked channel counts
+TRAIN_STEP_BASE = dict(TRAIN_STEP, Tx=20, Ty=100, x_lengths=[20, 16], y_lengths=[100, 84])
+# the tiny step with the MR-STFT loss weight 0 (train_stft.py:225, c_stft):
+# the L1 of log STFT magnitudes weights every bin by 1 / |X|, and any
+# waveform has near-zero bins, so under fp16 the waveform-path gradients are
+# dominated by rounding noise (tools/chaos_probe.py); without it the fp16
+# step's gradients are stable enough to be pinned per parameter
+TRAIN_STEP_ADV = dict(TRAIN_STEP, c_stft=0.0)
+TRAIN_VARIANTS = {
+    "train_step": (TRAIN_STEP, "tiny"),
+    "train_step_base": (TRAIN_STEP_BASE, "base"),
+    "train_step_adv": (TRAIN_STEP_ADV, "tiny"),
+}
+
+
+def train_step_inputs(c=None, data=None):
+    c = TRAIN_STEP if c is None else c
+    data = TINY_DATA if data is None else data
     g = torch.Generator().manual_seed(404)
     B, Tx, Ty = c["B"], c["Tx"], c["Ty"]
-    x = torch.randn(B, Tx, TINY_DATA["text_channels"], generator=g)
-    spec = torch.rand(B, TINY_DATA["spec_channels"], Ty, generator=g)
+    x = torch.randn(B, Tx, data["text_channels"], generator=g)
+    spec = torch.rand(B, data["spec_channels"], Ty, generator=g)
     y = (torch.randn(B, 1, Ty * c["hop"], generator=g) * 0.2).clamp(-1, 1)
     emo = torch.randn(B, 1024, generator=g)
     xl, yl = torch.tensor(c["x_lengths"]), torch.tensor(c["y_lengths"])
@@ -378,7 +399,7 @@ def train_step_inputs():
     return x, xl, spec, yl, y, yl * c["hop"], emo, torch.tensor(c["sid"])
 
 
-def make_train_step(models, stft_loss):
+def make_train_step(models, stft_loss, name="train_step"):
     import commons
     import losses
     import mrd
@@ -386,10 +407,17 @@ def make_train_step(models, stft_loss):
 
     from vits_amd.utils import deterministic_fill_sn_
 
-    c = TRAIN_STEP
-    cfg = dict(TINY, p_dropout=0.0, p_dropout_d=0.0)
-    net_g = models.SynthesizerTrn(TINY_DATA["text_channels"], TINY_DATA["spec_channels"],
-                                  c["seg_frames"], n_speakers=TINY_DATA["n_speakers"],
+    c, widths = TRAIN_VARIANTS[name]
+    if widths == "tiny":
+        cfg, data = dict(TINY, p_dropout=0.0, p_dropout_d=0.0), TINY_DATA
+    else:
+        bc = base_cfg()
+        cfg = dict(bc["model"], p_dropout=0.0, p_dropout_d=0.0)
+        data = dict(text_channels=bc["data"]["text_channels"],
+                    spec_channels=bc["data"]["filter_length"] // 2 + 1, segment_size=c["seg_frames"],
+                    n_speakers=bc["data"]["n_speakers"])
+    net_g = models.SynthesizerTrn(data["text_channels"], data["spec_channels"],
+                                  c["seg_frames"], n_speakers=data["n_speakers"],
                                   align_noise=c["align_noise"],
                                   align_noise_decay=c["align_noise_decay"], **cfg)
     deterministic_fill_(net_g)
@@ -404,7 +432,7 @@ def make_train_step(models, stft_loss):
     optim_d = radam.RAdam(net_d.parameters(), c["lr_d"])
     g0 = {k: p.detach().clone() for k, p in net_g.named_parameters()}
     d0 = {k: p.detach().clone() for k, p in net_d.named_parameters()}
-    x, xl, spec, sl, y, yl, emo, sid = train_step_inputs()
+    x, xl, spec, sl, y, yl, emo, sid = train_step_inputs(c, data)
     seg = c["seg_frames"]
     torch.manual_seed(777)
     with RecordRNG() as rec:
@@ -452,9 +480,9 @@ def make_train_step(models, stft_loss):
     for pre, grads, before, net in (("g_", g_grads, g0, net_g), ("d_", d_grads, d0, net_d)):
         arrs.update(_param_stats(grads, dict(net.named_parameters()), before, pre))
     arrs.update(_sn_state(net_d, "d_"))
-    np.savez_compressed(os.path.join(HERE, "train_step.npz"), **arrs)
-    with open(os.path.join(HERE, "train_step_config.json"), "w") as f:
-        json.dump(dict(step=c, model=cfg, data=TINY_DATA), f, indent=1)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+    with open(os.path.join(HERE, name + "_config.json"), "w") as f:
+        json.dump(dict(step=c, model=cfg, data=data), f, indent=1)
 
 
 def c1_inputs():
@@ -573,6 +601,8 @@ def main():
         for name in sys.argv[1:]:
             {"mpd": lambda: make_mpd(models), "mwsd": lambda: make_mwsd(stft_loss),
              "train_step": lambda: make_train_step(models, stft_loss),
+             "train_step_base": lambda: make_train_step(models, stft_loss, "train_step_base"),
+             "train_step_adv": lambda: make_train_step(models, stft_loss, "train_step_adv"),
              "c1": lambda: make_c1(models), "c5": lambda: make_c5(models)}[name]()
         return
     m = make_base(models)
@@ -582,7 +612,8 @@ def main():
     make_mrstft(stft_loss)
     make_mpd(models)
     make_mwsd(stft_loss)
-    make_train_step(models, stft_loss)
+    for name in TRAIN_VARIANTS:
+        make_train_step(models, stft_loss, name)
     with open(os.path.join(HERE, "tiny_config.json"), "w") as f:
         json.dump(dict(model=TINY, data=TINY_DATA), f, indent=1)
     print("golden fixtures written to", HERE)
