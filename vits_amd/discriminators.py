@@ -247,6 +247,20 @@ class GroupedSpectralNorm:
                 for m, n, _ in self.flat)
         return self._fused
 
+    def weights_pair(self):
+        """The W / sigma lists of two consecutive training-mode forwards (two
+        power iterations) from ONE autograd node (wnorm.spectral_norm_all2),
+        or None where the fused path does not apply."""
+        if not self._fused_ok():
+            return None
+        Ws = [getattr(m, n + "_orig") for m, n, _ in self.flat]
+        layers = [(getattr(m, n + "_u"), getattr(m, n + "_v"), eps) for m, n, eps in self.flat]
+        return wnorm.spectral_norm_all2(Ws, layers, self.cl16)
+
+    def set(self, ws):
+        for (m, n, _), w in zip(self.flat, ws):
+            setattr(m, n, w)
+
     def apply(self, training: bool):
         if self._fused_ok():
             Ws = [getattr(m, n + "_orig") for m, n, _ in self.flat]
@@ -298,6 +312,22 @@ class MultiWaveSTFTDiscriminator(nn.Module):
         # one launch (instead of one pack per conv call)
         with train_ops.prepacked(self):
             return self.mwd(x) + self.mfd(m)
+
+    def forward_pair(self, x1, m1, x2, m2):
+        """(forward(x1, m1), forward(x2, m2)) - the D(real) / D(fake) calls of
+        train_stft.py:198-200, in that order - with both passes' spectral
+        norms (two power iterations, as the two calls make) from one autograd
+        node, whose backward sums the two passes' weight gradients in one
+        multi-tensor add (two nodes: one add per layer, 85)."""
+        pair = self._sn.weights_pair() if self.training else None
+        if pair is None:
+            return self(x1, m1), self(x2, m2)
+        out = []
+        for ws, x, m in zip(pair, (x1, x2), (m1, m2)):
+            self._sn.set(ws)
+            with train_ops.prepacked(self):
+                out.append(self.mwd(x) + self.mfd(m))
+        return out[0], out[1]
 
 
 # ---------------------------------------------------------------------------

@@ -299,8 +299,13 @@ class TrainStep:
                 y = commons.slice_segments(y, ids_slice * hps.data.hop_length, hps.train.segment_size)
                 sc_loss, mag_loss, y_mag, y_hat_mag = self.mstft(y.squeeze(1), y_hat.squeeze(1))
             with rf("step:D.forward(real,fake)"):
-                y_d_hat_r = self.net_d(y, y_mag)
-                y_d_hat_g = self.net_d(y_hat.detach(), [m.detach() for m in y_hat_mag])
+                if isinstance(self.net_d, MultiWaveSTFTDiscriminator):
+                    # (one spectral-norm node for both passes; DDP keeps two calls)
+                    y_d_hat_r, y_d_hat_g = self.net_d.forward_pair(
+                        y, y_mag, y_hat.detach(), [m.detach() for m in y_hat_mag])
+                else:
+                    y_d_hat_r = self.net_d(y, y_mag)
+                    y_d_hat_g = self.net_d(y_hat.detach(), [m.detach() for m in y_hat_mag])
                 with self.autocast(False):
                     loss_disc, _, _ = discriminator_loss(y_d_hat_r, y_d_hat_g)
         with rf("step:D.backward"):

@@ -163,34 +163,70 @@ class WeightNormCache:
 # ---------------------------------------------------------------------------
 
 
+def _sn_forward(layers, training: bool, emu16: bool, Ws):
+    """One launch: (outs, saved, offs, shapes) of W / sigma(W) for every W
+    (power iteration on the layers' u / v buffers when training)."""
+    n = len(Ws)
+    # layers: (u, v, eps, cl) - cl = C > 0: W / sigma as the fp16
+    # channels-last image the autocast MIOpen conv would cast it to
+    outs = [torch.empty(W.shape, device=W.device, dtype=torch.float16,
+                        memory_format=torch.channels_last) if lay[3] else torch.empty_like(W)
+            for W, lay in zip(Ws, layers)]
+    shapes = [(W.shape[0], W.numel() // W.shape[0]) for W in Ws]
+    offs, tot = [], 0
+    for r, c in shapes:
+        offs.append(tot)
+        tot += 1 + r + c
+    saved = torch.empty(tot, device=Ws[0].device, dtype=torch.float32)
+    arr = (SnormLayer * n)()
+    for i, (W, (u, v, eps, cl)) in enumerate(zip(Ws, layers)):
+        e = arr[i]
+        e.w, e.u, e.v, e.w_sn = W.data_ptr(), u.data_ptr(), v.data_ptr(), outs[i].data_ptr()
+        e.saved = saved.data_ptr() + 4 * offs[i]
+        e.rows, e.cols = shapes[i]
+        e.eps = eps
+        e.cl_channels = cl
+    check(_lib.load().vits_spectral_norm_forward(arr, n, int(training), int(emu16),
+                                                 _stream(saved)), "vits_spectral_norm_forward")
+    return outs, saved, offs, shapes
+
+
+def _sn_backward(Ws, saved, offs, shapes, emu16, cls, gs, need):
+    """dW of W / sigma(W) for the layers with a gradient (one launch)."""
+    n = len(Ws)
+    dWs = [None] * n
+    idx = [i for i in range(n) if gs[i] is not None and need[i]]
+    if idx:
+        arr = (SnormLayer * len(idx))()
+        keep = []
+        for a, i in enumerate(idx):
+            if cls[i]:
+                g = gs[i].to(torch.float16).contiguous(memory_format=torch.channels_last)
+            else:
+                g = gs[i].float().contiguous()
+            keep.append(g)
+            dWs[i] = torch.empty_like(Ws[i])
+            e = arr[a]
+            e.w, e.dw_sn, e.dw = Ws[i].data_ptr(), g.data_ptr(), dWs[i].data_ptr()
+            e.saved = saved.data_ptr() + 4 * offs[i]
+            e.rows, e.cols = shapes[i]
+            e.cl_channels = cls[i]
+        lib = _lib.load()
+        nws = lib.vits_spectral_norm_workspace(arr, len(idx))
+        ws = torch.empty(max(1, nws), device=saved.device, dtype=torch.float32)
+        check(lib.vits_spectral_norm_backward(arr, len(idx), int(emu16), ws.data_ptr(),
+                                              ws.numel(), _stream(saved)),
+              "vits_spectral_norm_backward")
+    return dWs
+
+
 class _SpectralNormAll(torch.autograd.Function):
     """(W_0..W_{n-1}) -> (W_0 / sigma_0, ...); power iteration on the u / v
-    buffers of ``layers`` (a list of (u, v, eps)) in training mode."""
+    buffers of ``layers`` (a list of (u, v, eps, cl)) in training mode."""
 
     @staticmethod
     def forward(ctx, layers, training: bool, emu16: bool, *Ws):
-        n = len(Ws)
-        # layers: (u, v, eps, cl) - cl = C > 0: W / sigma as the fp16
-        # channels-last image the autocast MIOpen conv would cast it to
-        outs = [torch.empty(W.shape, device=W.device, dtype=torch.float16,
-                            memory_format=torch.channels_last) if lay[3] else torch.empty_like(W)
-                for W, lay in zip(Ws, layers)]
-        shapes = [(W.shape[0], W.numel() // W.shape[0]) for W in Ws]
-        offs, tot = [], 0
-        for r, c in shapes:
-            offs.append(tot)
-            tot += 1 + r + c
-        saved = torch.empty(tot, device=Ws[0].device, dtype=torch.float32)
-        arr = (SnormLayer * n)()
-        for i, (W, (u, v, eps, cl)) in enumerate(zip(Ws, layers)):
-            e = arr[i]
-            e.w, e.u, e.v, e.w_sn = W.data_ptr(), u.data_ptr(), v.data_ptr(), outs[i].data_ptr()
-            e.saved = saved.data_ptr() + 4 * offs[i]
-            e.rows, e.cols = shapes[i]
-            e.eps = eps
-            e.cl_channels = cl
-        check(_lib.load().vits_spectral_norm_forward(arr, n, int(training), int(emu16),
-                                                     _stream(saved)), "vits_spectral_norm_forward")
+        outs, saved, offs, shapes = _sn_forward(layers, training, emu16, Ws)
         ctx.offs, ctx.shapes, ctx.emu16 = offs, shapes, emu16
         ctx.cls = [lay[3] for lay in layers]
         ctx.set_materialize_grads(False)
@@ -202,37 +238,61 @@ class _SpectralNormAll(torch.autograd.Function):
     def backward(ctx, *gs):
         saved_t = ctx.saved_tensors
         Ws, saved = saved_t[:-1], saved_t[-1]
-        n = len(Ws)
-        dWs = [None] * n
-        idx = [i for i in range(n) if gs[i] is not None and ctx.needs_input_grad[3 + i]]
-        if idx:
-            arr = (SnormLayer * len(idx))()
-            keep = []
-            for a, i in enumerate(idx):
-                if ctx.cls[i]:
-                    g = gs[i].to(torch.float16).contiguous(memory_format=torch.channels_last)
-                else:
-                    g = gs[i].float().contiguous()
-                keep.append(g)
-                dWs[i] = torch.empty_like(Ws[i])
-                e = arr[a]
-                e.w, e.dw_sn, e.dw = Ws[i].data_ptr(), g.data_ptr(), dWs[i].data_ptr()
-                e.saved = saved.data_ptr() + 4 * ctx.offs[i]
-                e.rows, e.cols = ctx.shapes[i]
-                e.cl_channels = ctx.cls[i]
-            lib = _lib.load()
-            nws = lib.vits_spectral_norm_workspace(arr, len(idx))
-            ws = torch.empty(max(1, nws), device=saved.device, dtype=torch.float32)
-            check(lib.vits_spectral_norm_backward(arr, len(idx), int(ctx.emu16), ws.data_ptr(),
-                                                  ws.numel(), _stream(saved)),
-                  "vits_spectral_norm_backward")
+        dWs = _sn_backward(Ws, saved, ctx.offs, ctx.shapes, ctx.emu16, ctx.cls, gs,
+                           ctx.needs_input_grad[3:])
         return (None, None, None, *dWs)
+
+
+class _SpectralNormAll2(torch.autograd.Function):
+    """Two consecutive training-mode spectral norms of the same weights (the
+    D(real) and D(fake) forwards of train_stft.py:198-200, one power
+    iteration each) as ONE autograd node: (W_0..W_{n-1}) -> (W_i / sigma1_i
+    for every i, then W_i / sigma2_i for every i).  Its backward runs one
+    backward launch per pass and sums them with one multi-tensor add, where
+    two nodes would make autograd add each layer's two gradients one by one."""
+
+    @staticmethod
+    def forward(ctx, layers, emu16: bool, *Ws):
+        outs1, saved1, offs, shapes = _sn_forward(layers, True, emu16, Ws)
+        outs2, saved2, _, _ = _sn_forward(layers, True, emu16, Ws)
+        ctx.offs, ctx.shapes, ctx.emu16 = offs, shapes, emu16
+        ctx.cls = [lay[3] for lay in layers]
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(*Ws, saved1, saved2)
+        return tuple(outs1) + tuple(outs2)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, *gs):
+        n = len(gs) // 2
+        saved_t = ctx.saved_tensors
+        Ws, saved1, saved2 = saved_t[:n], saved_t[n], saved_t[n + 1]
+        need = ctx.needs_input_grad[2:]
+        d1 = _sn_backward(Ws, saved1, ctx.offs, ctx.shapes, ctx.emu16, ctx.cls, gs[:n], need)
+        d2 = _sn_backward(Ws, saved2, ctx.offs, ctx.shapes, ctx.emu16, ctx.cls, gs[n:], need)
+        both = [i for i in range(n) if d1[i] is not None and d2[i] is not None]
+        if both:
+            torch._foreach_add_([d1[i] for i in both], [d2[i] for i in both])
+        return (None, None, *[d1[i] if d1[i] is not None else d2[i] for i in range(n)])
 
 
 def spectral_norm_supported(W: torch.Tensor) -> bool:
     if not (W.is_cuda and W.dtype == torch.float32 and W.is_contiguous() and W.dim() >= 2):
         return False
     return bool(_lib.load().vits_spectral_norm_supported(W.shape[0], W.numel() // W.shape[0]))
+
+
+def spectral_norm_all2(Ws, layers, cl16=None):
+    """spectral_norm_all twice in training mode (two power iterations, the
+    u / v buffers updated by each) as one autograd node: (the first pass's
+    W / sigma list, the second pass's)."""
+    dev = Ws[0].device.type
+    emu16 = torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.float16
+    cl16 = cl16 or [False] * len(Ws)
+    lay = [(u, v, eps, W.shape[1] if (emu16 and c and W.dim() == 4) else 0)
+           for W, (u, v, eps), c in zip(Ws, layers, cl16)]
+    outs = _SpectralNormAll2.apply(lay, bool(emu16), *Ws)
+    return list(outs[:len(Ws)]), list(outs[len(Ws):])
 
 
 def spectral_norm_all(Ws, layers, training: bool, cl16=None):
@@ -257,4 +317,5 @@ def spectral_norm_hook(m: torch.nn.Module, name: str):
     return None
 
 
-__all__ = ["WeightNormCache", "spectral_norm_all", "spectral_norm_supported", "FUSED_NORMS"]
+__all__ = ["WeightNormCache", "spectral_norm_all", "spectral_norm_all2", "spectral_norm_supported",
+           "FUSED_NORMS"]
