@@ -10,6 +10,7 @@ MultiWaveSTFTDiscriminator 200-236.
 """
 from __future__ import annotations
 
+import contextlib
 
 import torch
 import torch.nn as nn
@@ -121,7 +122,9 @@ class STFTDiscriminator(nn.Module):
             for layer in layers:
                 if isinstance(layer, Conv2d):
                     w = layer.weight
-                    h = F.conv2d(h, w.contiguous(memory_format=torch.channels_last), layer.bias,
+                    b = layer.__dict__.get("_vits_b16")
+                    h = F.conv2d(h, w.contiguous(memory_format=torch.channels_last),
+                                 layer.bias if b is None else b,
                                  layer.stride, layer.padding, layer.dilation, layer.groups)
                 else:
                     h = layer(h)
@@ -310,8 +313,29 @@ class MultiWaveSTFTDiscriminator(nn.Module):
         self._sn.apply(self.training)
         # every HIP conv's 16-bit images from the W / sigma just computed, in
         # one launch (instead of one pack per conv call)
-        with train_ops.prepacked(self):
+        with train_ops.prepacked(self), self._biases16():
             return self.mwd(x) + self.mfd(m)
+
+    @contextlib.contextmanager
+    def _biases16(self):
+        """Under fp16 autocast on the GPU: the STFT discriminators' MIOpen
+        Conv2d biases cast to fp16 by ONE cat + cast (autocast casts each
+        conv's bias on every call: 30 casts per forward and their backwards)."""
+        dev = "cuda"
+        convs = [c for d in self.mfd.discriminators for c in d.convs
+                 if isinstance(c, Conv2d) and c.bias is not None and c.bias.is_cuda]
+        if (not convs or not STFT_D_NHWC or not torch.is_autocast_enabled(dev)
+                or torch.get_autocast_dtype(dev) != torch.float16):
+            yield
+            return
+        b16 = torch.cat([c.bias for c in convs]).half().split([c.bias.numel() for c in convs])
+        for c, b in zip(convs, b16):
+            c.__dict__["_vits_b16"] = b
+        try:
+            yield
+        finally:
+            for c in convs:
+                c.__dict__.pop("_vits_b16", None)
 
     def forward_pair(self, x1, m1, x2, m2):
         """(forward(x1, m1), forward(x2, m2)) - the D(real) / D(fake) calls of
@@ -323,10 +347,11 @@ class MultiWaveSTFTDiscriminator(nn.Module):
         if pair is None:
             return self(x1, m1), self(x2, m2)
         out = []
-        for ws, x, m in zip(pair, (x1, x2), (m1, m2)):
-            self._sn.set(ws)
-            with train_ops.prepacked(self):
-                out.append(self.mwd(x) + self.mfd(m))
+        with self._biases16():
+            for ws, x, m in zip(pair, (x1, x2), (m1, m2)):
+                self._sn.set(ws)
+                with train_ops.prepacked(self):
+                    out.append(self.mwd(x) + self.mfd(m))
         return out[0], out[1]
 
 

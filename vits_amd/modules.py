@@ -74,18 +74,19 @@ class WN(nn.Module):
         H = self.hidden_channels
         output = None  # zeros_like(x), materialised on first use
         g32 = None
+        H2 = 2 * H
         if self.gin_channels != 0:
             g = train_ops.linear(self.cond_layer, g)
             g32 = train_ops.cond_f32(g)  # one cast for every layer's fused gate
+            if g32 is not None:  # the layers' slices, with a one-launch backward
+                g32 = train_ops.split_cols(g32, self.n_layers, H2)
         x16 = None  # x rounded to the conv dtype by the fused update (WNUpdate16)
         for i in range(self.n_layers):
             xi = x if x16 is None else x16
-            H2 = 2 * H
             g_l = g[:, i * H2:(i + 1) * H2] if self.gin_channels else None
             # in_layer conv + gate as one launch on the fp16 training path
             if g32 is not None:
-                acts = train_ops.conv1d_gate(self.in_layers[i], xi, g32[:, i * H2:(i + 1) * H2],
-                                             g16=g_l)
+                acts = train_ops.conv1d_gate(self.in_layers[i], xi, g32[i], g16=g_l)
             else:
                 acts = train_ops.conv1d_gate(self.in_layers[i], xi, g_l)
             if acts is None:

@@ -1097,6 +1097,35 @@ class ConvGateHip16(torch.autograd.Function):
 COND_F32 = True
 
 
+class _SplitCols(torch.autograd.Function):
+    """x[:, i*w:(i+1)*w] for i < n as views; the backward concatenates the n
+    column gradients in ONE launch (n slice backwards would each allocate a
+    zero tensor of x's size, copy into it and add: 3n - 1 launches)."""
+
+    @staticmethod
+    def forward(ctx, x, n: int, w: int):
+        ctx.shape, ctx.dtype = x.shape, x.dtype
+        ctx.set_materialize_grads(False)
+        return tuple(x[:, i * w:(i + 1) * w] for i in range(n))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        B = ctx.shape[0]
+        w = ctx.shape[1] // len(gs)
+        parts = [g if g is not None else
+                 torch.zeros(B, w, device=next(t for t in gs if t is not None).device,
+                             dtype=ctx.dtype) for g in gs]
+        return torch.cat(parts, 1), None, None
+
+
+def split_cols(x: torch.Tensor, n: int, w: int):
+    """The n column blocks of width w of x [B, n * w] (the per-layer cond
+    slices of modules.WN, modules.py:141-142), with a one-launch backward."""
+    if not x.requires_grad or x.shape[1] != n * w:
+        return [x[:, i * w:(i + 1) * w] for i in range(n)]
+    return list(_SplitCols.apply(x, n, w))
+
+
 def cond_f32(g: torch.Tensor | None):
     """fp32 copy of a 16-bit cond tensor (every layer's slice then feeds the
     fused gate's fp32 epilogue without a cast of its own), or None when the
