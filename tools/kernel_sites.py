@@ -45,6 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--top", type=int, default=90)
+    ap.add_argument("--shapes", action="store_true", help="print the input shapes per site")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     hps = default_hps()
@@ -56,11 +57,13 @@ def main():
         st.step(batch)
     torch.cuda.synchronize()
     print("warm", flush=True)
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 record_shapes=True) as prof:
         st.step(batch)
         torch.cuda.synchronize()
     rows = collections.defaultdict(lambda: [0, 0.0])
     fams = collections.defaultdict(lambda: [0, 0.0])
+    shapes = collections.defaultdict(collections.Counter)
     for ev in prof.events():
         for k in getattr(ev, "kernels", []) or []:
             f = family(k.name)
@@ -69,6 +72,8 @@ def main():
             rows[key][1] += k.duration / 1e3
             fams[f][0] += 1
             fams[f][1] += k.duration / 1e3
+            if a.shapes:
+                shapes[key][str(getattr(ev, "input_shapes", ""))[:90]] += 1
     n = sum(v[0] for v in fams.values())
     ms = sum(v[1] for v in fams.values())
     print(f"kernels in one eager step: {n} dispatches, {ms:.2f} ms device time")
@@ -78,6 +83,9 @@ def main():
     print("-- by site")
     for (s, f), (c, t) in sorted(rows.items(), key=lambda kv: -kv[1][0])[:a.top]:
         print(f"{c:6d} {t:9.3f} ms  {f:22s} {s}")
+        if a.shapes:
+            for shp, n in shapes[(s, f)].most_common(3):
+                print(f"{'':20s} {n:4d} x {shp}")
 
 
 if __name__ == "__main__":
