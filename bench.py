@@ -464,8 +464,9 @@ def train_leg(args, device, rank, world, dist, B=None, cpu_base=True):
     torch.manual_seed(hps.train.seed)
     net_g, net_d = build_models(hps, device)
     # the whole step replayed from one hipGraph (TrainStep.capture); with
-    # several ranks the gradient average is one flat RCCL all-reduce per
-    # network captured in the graph (allreduce=True; DDP's hooks are not
+    # several ranks G's gradients are averaged in nine ordered RCCL buckets
+    # on a side stream as each bucket completes, D's in one flat all-reduce,
+    # all captured in the graph (allreduce=True; DDP's hooks are not
     # capturable, so the eager path keeps DDP)
     use_graph = not args.train_eager
     st = TrainStep(hps, net_g, net_d, device, ddp=world > 1 and not use_graph,
@@ -503,7 +504,8 @@ def train_leg(args, device, rank, world, dist, B=None, cpu_base=True):
            "scaling": "weak",
            "workload": f"train_stft step (G fwd/bwd + MWSD D x3 + MR-STFT + MAS) batch={B}/GPU "
                        f"Tx={args.tx} Ty={args.ty} segment 48 frames",
-           "parallelism": (f"dp{world} (flat RCCL all-reduce per network)" if st.allreduce else
+           "parallelism": (f"dp{world} (G: 9 overlapped RCCL buckets, D: one flat all-reduce)"
+                            if st.allreduce else
                            f"ddp{world} (RCCL all-reduce)") if world > 1 else "single GPU",
            "graph": use_graph,
            "tflops_alg": round(TRAIN_GFLOP_PER_UTT * 1e9 * utt / el / 1e12, 2),
