@@ -462,6 +462,11 @@ def train_leg(args, device, rank, world, dist, B=None, cpu_base=True):
 
     hps = default_hps()
     torch.manual_seed(hps.train.seed)
+    # train_stft.py:26 sets cudnn.benchmark: MIOpen's exhaustive find for the
+    # STFT discriminators' Conv2d layers (the step's only MIOpen convs) picks
+    # faster solvers than its default find (69.2 -> 67.0 ms per B=32 step,
+    # profiles/r06_cudnn_benchmark_ab.txt); the search runs in the warm-up
+    torch.backends.cudnn.benchmark = True
     net_g, net_d = build_models(hps, device)
     # the whole step replayed from one hipGraph (TrainStep.capture); with
     # several ranks G's gradients are averaged in nine ordered RCCL buckets
