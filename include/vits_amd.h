@@ -647,6 +647,59 @@ int vits_wn_update_backward(const float* gx, const void* gx16, const float* gout
                             const float* mask, float* dx, void* drs, int batch, int H, int T,
                             int wdtype, void* stream);
 
+/* ---------------------------------------------------------------------- */
+/* Mean-only coupling layer glue of the fp16-autocast training step       */
+/* (ResidualCouplingLayer.forward modules.py:314-360, WN output           */
+/* modules.py:182, Flip folded in: ResidualCouplingBlock models.py:219-235).*/
+/* mask_cast: h = y * mask (fp32) and h16 = h in the 16-bit type;          */
+/*   backward: dy = 16-bit((gh + gh16) * mask) (either NULL = 0).         */
+/* wn_final: o16 = 16-bit((out + rs) * mask) (out NULL = 0); backward:    */
+/*   d = g16 * mask, dout = d (fp32, NULL = skip), drs = 16-bit(d).       */
+/* coupling: x [B][2h][T] fp32, p = post conv output [B][h][T] 16-bit,    */
+/*   m = p * mask; out = cat(x0, reverse ? (x1 - m) * mask :              */
+/*   m + x1 * mask), channel-reversed when flip; backward: gx0 = g0, gx1 = */
+/*   g1 * mask, gp = 16-bit(+-g1 * mask) (g read through the same flip).  */
+/* ---------------------------------------------------------------------- */
+int vits_mask_cast_forward(const void* y, const float* mask, float* h, void* h16, int batch,
+                           int C, int T, int wdtype, void* stream);
+int vits_mask_cast_backward(const float* gh, const void* gh16, const float* mask, void* dy,
+                            int batch, int C, int T, int wdtype, void* stream);
+int vits_wn_final_forward(const float* out, const void* rs, const float* mask, void* o16,
+                          int batch, int C, int T, int wdtype, void* stream);
+int vits_wn_final_backward(const void* g16, const float* mask, float* dout, void* drs, int batch,
+                           int C, int T, int wdtype, void* stream);
+int vits_coupling_forward(const float* x, const void* p, const float* mask, float* out,
+                          int batch, int half, int T, int reverse, int flip, int wdtype,
+                          void* stream);
+int vits_coupling_backward(const float* g, const float* mask, float* gx, void* gp, int batch,
+                           int half, int T, int reverse, int flip, int wdtype, void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* STFT-discriminator glue of the fp16-autocast training step             */
+/* (mrd.py:94-156, STFTDiscriminator.forward: Conv2d -> LeakyReLU ...).   */
+/* join_to_cl: the first layer's joined-row conv output y [B][C][F_out*L] */
+/* (row f's T outputs at columns f*L + p1 ..) -> out [B][F_out][T][C]     */
+/* (NHWC) = leaky_relu(y, slope); backward: dy [B][C][F_out*L] =          */
+/* lrelu'(out) * g at output columns, 0 at pad columns.                   */
+/* bias_lrelu: out = leaky_relu(y + fp16(bias), slope) on NHWC rows of C  */
+/* channels (the MIOpen conv runs without bias); backward: dy = lrelu'(out)*g */
+/* and db[c] = fp16-rounded fp32 sum of dy (deterministic: per-workgroup  */
+/* partials in `workspace`, added in workgroup order by a second launch). */
+/* 16-bit tensors of `wdtype`; C % 8 == 0, C <= 512 (bias_lrelu backward: */
+/* 256 % (C/8) == 0).                                                      */
+/* ---------------------------------------------------------------------- */
+int vits_stftd_join_to_cl_forward(const void* y, void* out, int batch, int C, int F_out, int L,
+                                  int p1, int T, float slope, int wdtype, void* stream);
+int vits_stftd_join_to_cl_backward(const void* g, const void* out, void* dy, int batch, int C,
+                                   int F_out, int L, int p1, int T, float slope, int wdtype,
+                                   void* stream);
+int vits_bias_lrelu_forward(const void* y, const float* bias, void* out, int64_t rows, int C,
+                            float slope, int wdtype, void* stream);
+int vits_bias_lrelu_workspace(int64_t rows, int C);
+int vits_bias_lrelu_backward(const void* g, const void* out, void* dy, float* db,
+                             float* workspace, int ws_floats, int64_t rows, int C, float slope,
+                             int wdtype, void* stream);
+
 /* library introspection */
 const char* vits_amd_version(void);
 int vits_amd_device_arch(char* buf, int len);

@@ -698,3 +698,119 @@ def test_resblock_stage_grouped_matches_per_branch(device, monkeypatch):
         worst.append((eb - ea, n, ea, eb))
         assert eb <= 1.25 * ea + 1e-4 and rl2(gb[n], ga[n]) < 1e-2, (n, ea, eb)
     print("largest grouped-minus-per-branch error vs fp32:", sorted(worst)[-3:])
+
+
+@pytest.mark.parametrize("B,C,F_out,T,p1", [(2, 64, 61, 19, 2), (3, 64, 7, 289, 2),
+                                           (1, 8, 5, 3, 0), (2, 128, 33, 37, 1)])
+def test_stftd_join_to_cl(device, B, C, F_out, T, p1):
+    """discriminators._JoinToCL (stftd.hip join_to_cl) against torch's slice
+    of the joined rows + channels-last copy + leaky_relu on the same fp16
+    tensor: the output and the joined-row data gradient (zeros at the pad
+    columns) bit-equal to torch autograd's."""
+    import vits_amd.discriminators as D
+
+    g = torch.Generator().manual_seed(B * 100 + C + F_out)
+    L = (T + 2 * p1 + 3) // 4 * 4
+    y = torch.randn(B, C, F_out * L, generator=g).half().to(device)
+    y[:, :, :5] = 0  # (zeros through the activation)
+    yd = y.clone().requires_grad_(True)
+    out = D._JoinToCL.apply(yd, F_out, L, p1, T, 0.2)
+    yr = y.clone().requires_grad_(True)
+    ref = F.leaky_relu(yr.view(B, C, F_out, L)[..., p1:p1 + T], 0.2).contiguous(
+        memory_format=torch.channels_last)
+    assert out.shape == ref.shape and out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out, ref)
+    dy = torch.randn(B, C, F_out, T, generator=g).half().to(device)
+    out.backward(dy)
+    ref.backward(dy)
+    assert torch.equal(yd.grad, yr.grad)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 64, 29, 37), (3, 64, 1, 19), (1, 32, 3, 5),
+                                     (4, 128, 13, 73)])
+def test_bias_lrelu_cl(device, B, C, H, W):
+    """discriminators.bias_lrelu_cl (stftd.hip bias_lrelu) against torch's
+    conv-bias add + leaky_relu on a channels-last fp16 tensor: output and
+    data gradient bit-equal; the bias gradient (fp32 sum, rounded through
+    fp16 as the reference's fp16 bias gradient) within one fp16 ulp of the
+    fp64 sum, and identical run to run (ordered partials)."""
+    import vits_amd.discriminators as D
+
+    g = torch.Generator().manual_seed(B * 10 + C + H)
+    y = torch.randn(B, C, H, W, generator=g).half().to(device).contiguous(
+        memory_format=torch.channels_last)
+    bias = (torch.randn(C, generator=g) * 0.3).to(device).requires_grad_(True)
+    yd = y.clone().requires_grad_(True)
+    out = D.bias_lrelu_cl(yd, bias, 0.2)
+    yr = y.clone().requires_grad_(True)
+    br = bias.detach().clone().requires_grad_(True)
+    ref = F.leaky_relu(yr + br.half().view(1, C, 1, 1), 0.2)
+    assert torch.equal(out, ref)
+    dy = torch.randn(B, C, H, W, generator=g).half().to(device).contiguous(
+        memory_format=torch.channels_last)
+    out.backward(dy)
+    ref.backward(dy)
+    assert torch.equal(yd.grad, yr.grad)
+    d16 = yr.grad.double().sum((0, 2, 3))
+    ulp = d16.abs().half().float().double() * 2.0 ** -10 + 1e-6
+    assert ((bias.grad.double() - d16).abs() <= ulp.to(device)).all()
+    g1 = bias.grad.clone()
+    bias.grad = None
+    D.bias_lrelu_cl(y.clone().requires_grad_(True), bias, 0.2).backward(dy)
+    assert torch.equal(bias.grad, g1)
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+def test_coupling_block_fused_matches_reference_ops(reverse):
+    """ResidualCouplingBlock under fp16 autocast with the coupling glue on
+    wnres.hip (mask_cast, wn_final, the coupling update with the Flip folded
+    in) vs the reference's op sequence (models.py:219-235, modules.py:314-360:
+    pre * mask, WN output * mask, exp(logs = 0), cat, Flip) on the same HIP
+    convs: the output, the input gradient and every parameter gradient
+    bit-equal (the fused kernels round where autocast does; x1 * exp(0) is
+    x1 exactly)."""
+    from vits_amd import models
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(11)
+    B, C, H, T, gin = 2, 16, 32, 157, 24
+    blk = models.ResidualCouplingBlock(C, H, 5, [1, 1, 1, 1], 4, n_flows=4,
+                                       gin_channels=gin).to(dev)
+    with torch.no_grad():
+        for f in blk.flows:
+            if hasattr(f, "post"):  # (zero-initialised in the reference)
+                f.post.weight.normal_(0, 0.05)
+                f.post.bias.normal_(0, 0.05)
+    x = torch.randn(B, C, T, device=dev)
+    g = torch.randn(B, gin, device=dev)
+    mask = torch.ones(B, 1, T, device=dev)
+    mask[1, :, 120:] = 0
+    w = torch.randn(B, C, T, device=dev)
+
+    def run(fused):
+        old = train_ops.COUPLING_FUSED
+        train_ops.COUPLING_FUSED = fused
+        try:
+            blk.zero_grad(set_to_none=True)
+            xs = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.float16):
+                if fused:
+                    y = blk(xs, mask, g=g, reverse=reverse)
+                else:  # the reference's loop: coupling, then the Flip module
+                    y = xs
+                    for f in (blk.flows if not reverse else list(blk.flows)[::-1]):
+                        if reverse:
+                            y = f(y, mask, g=g, reverse=True)
+                        else:
+                            y, _ = f(y, mask, g=g)
+            (y * w).sum().backward()
+            return [y.detach(), xs.grad] + [p.grad.clone() for p in blk.parameters()
+                                            if p.grad is not None]
+        finally:
+            train_ops.COUPLING_FUSED = old
+
+    got, want = run(True), run(False)
+    assert len(got) == len(want)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert a.dtype == b.dtype and a.shape == b.shape, i
+        assert torch.equal(a, b), (i, (a.float() - b.float()).abs().max().item())

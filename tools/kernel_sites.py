@@ -46,8 +46,17 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--top", type=int, default=90)
     ap.add_argument("--shapes", action="store_true", help="print the input shapes per site")
+    ap.add_argument("--set", action="append", default=[], help="module.CONST=int (A/B)")
     a = ap.parse_args()
+    import importlib
+
+    for kv in a.set:
+        k, v = kv.split("=")
+        mod, attr = k.rsplit(".", 1)
+        m = importlib.import_module("vits_amd." + mod)
+        setattr(m, attr, type(getattr(m, attr))(int(v)))
     dev = torch.device("cuda:0")
+    torch.backends.cudnn.benchmark = True  # as bench.py's train legs (train_stft.py:26)
     hps = default_hps()
     torch.manual_seed(hps.train.seed)
     net_g, net_d = build_models(hps, dev)

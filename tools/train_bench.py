@@ -27,7 +27,16 @@ def main():
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="torch.backends.cudnn.benchmark = True (train_stft.py:26)")
     ap.add_argument("--variant", choices=["stft", "mel"], default="stft")
+    ap.add_argument("--set", action="append", default=[],
+                    help="module.CONST=int for an in-process A/B, e.g. discriminators.STFT_D_FUSED=0")
     args = ap.parse_args()
+    import importlib
+
+    for kv in args.set:
+        k, v = kv.split("=")
+        mod, attr = k.rsplit(".", 1)
+        setattr(importlib.import_module("vits_amd." + mod), attr, type(getattr(
+            importlib.import_module("vits_amd." + mod), attr))(int(v)))
     dev = torch.device("cuda:0")
     torch.backends.cudnn.benchmark = args.cudnn_benchmark
     hps = default_hps()
@@ -68,7 +77,7 @@ def main():
             phases = [e for e in ka if e.key.startswith("step:")]
             for e in sorted(phases, key=lambda e: -e.device_time_total):
                 f.write(f"{e.key:32s} device {e.device_time_total / 1e3:8.2f} ms  cpu {e.cpu_time_total / 1e3:8.2f} ms\n")
-    print(json.dumps({"variant": args.variant, "batch": args.batch, "s_per_step": dt, "utt_per_s": args.batch / dt,
+    print(json.dumps({"set": args.set, "variant": args.variant, "batch": args.batch, "s_per_step": dt, "utt_per_s": args.batch / dt,
                       "loss_g": float(out["loss_gen_all"]), "loss_d": float(out["loss_disc"]),
                       "max_mem_gb": torch.cuda.max_memory_allocated() / 2**30}), flush=True)
 

@@ -385,6 +385,22 @@ _SIGS = {
         C.c_int, [C.c_void_p] * 7 + [C.c_int] * 4 + [C.c_void_p]),
     "vits_wn_update_backward": (
         C.c_int, [C.c_void_p] * 6 + [C.c_int] * 4 + [C.c_void_p]),
+    "vits_mask_cast_forward": (C.c_int, [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_void_p]),
+    "vits_mask_cast_backward": (C.c_int, [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_void_p]),
+    "vits_wn_final_forward": (C.c_int, [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_void_p]),
+    "vits_wn_final_backward": (C.c_int, [C.c_void_p] * 4 + [C.c_int] * 4 + [C.c_void_p]),
+    "vits_coupling_forward": (C.c_int, [C.c_void_p] * 4 + [C.c_int] * 6 + [C.c_void_p]),
+    "vits_coupling_backward": (C.c_int, [C.c_void_p] * 4 + [C.c_int] * 6 + [C.c_void_p]),
+    "vits_stftd_join_to_cl_forward": (
+        C.c_int, [C.c_void_p] * 2 + [C.c_int] * 6 + [C.c_float, C.c_int, C.c_void_p]),
+    "vits_stftd_join_to_cl_backward": (
+        C.c_int, [C.c_void_p] * 3 + [C.c_int] * 6 + [C.c_float, C.c_int, C.c_void_p]),
+    "vits_bias_lrelu_forward": (
+        C.c_int, [C.c_void_p] * 3 + [C.c_int64, C.c_int, C.c_float, C.c_int, C.c_void_p]),
+    "vits_bias_lrelu_workspace": (C.c_int, [C.c_int64, C.c_int]),
+    "vits_bias_lrelu_backward": (
+        C.c_int, [C.c_void_p] * 5 + [C.c_int, C.c_int64, C.c_int, C.c_float, C.c_int,
+                                     C.c_void_p]),
     "vits_amd_version": (C.c_char_p, []),
     "vits_amd_device_arch": (C.c_int, [C.c_char_p, C.c_int]),
     "vits_dispatch_count": (C.c_int64, [C.c_int]),

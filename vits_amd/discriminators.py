@@ -19,8 +19,9 @@ from torch.nn import Conv1d, Conv2d, LeakyReLU
 from torch.nn.utils import spectral_norm, weight_norm
 from torch.nn.utils.spectral_norm import SpectralNorm
 
-from . import train_ops, wnorm
+from . import _lib, train_ops, wnorm
 from .commons import get_padding
+from .ops import _stream_ptr
 
 LRELU_SLOPE = 0.2
 
@@ -112,22 +113,42 @@ class STFTDiscriminator(nn.Module):
         # (16-bit autocast only: in fp32 training the 2-D layers stay MIOpen's)
         wdt = train_ops.train_wdtype(x)
         wdt = wdt if wdt in train_ops._TORCH_16 else None
+        fused = STFT_D_FUSED and wdt is not None and STFT_D_NHWC
         if STFT_D_HIP and wdt is not None and _freq_conv_ok(first):
             # the 1-channel first layer (its data-gradient was CK's slowest
             # conv kernel in the step) on the HIP training conv
-            h = conv2d_freq(first, h, wdt)
-            layers = layers[1:]
+            nxt = layers[1] if len(layers) > 1 else None
+            if fused and isinstance(nxt, LeakyReLU) and _lrelu_cl_ok(first.out_channels):
+                # its output sliced, made channels-last and activated in one
+                # kernel (stftd.hip join_to_cl)
+                h = conv2d_freq(first, h, wdt, out_slope=nxt.negative_slope)
+                layers = layers[2:]
+            else:
+                h = conv2d_freq(first, h, wdt)
+                layers = layers[1:]
         if STFT_D_NHWC and h.device.type == "cuda":
             h = h.contiguous(memory_format=torch.channels_last)
-            for layer in layers:
+            i = 0
+            while i < len(layers):
+                layer = layers[i]
                 if isinstance(layer, Conv2d):
-                    w = layer.weight
+                    w = layer.weight.contiguous(memory_format=torch.channels_last)
+                    nxt = layers[i + 1] if i + 1 < len(layers) else None
+                    if (fused and isinstance(nxt, LeakyReLU) and layer.bias is not None
+                            and _lrelu_cl_ok(layer.out_channels)):
+                        # bias + LeakyReLU (and, backward, the bias gradient)
+                        # in one kernel around the bias-less MIOpen conv
+                        y = F.conv2d(h, w, None, layer.stride, layer.padding, layer.dilation,
+                                     layer.groups)
+                        h = bias_lrelu_cl(y, layer.bias, nxt.negative_slope)
+                        i += 2
+                        continue
                     b = layer.__dict__.get("_vits_b16")
-                    h = F.conv2d(h, w.contiguous(memory_format=torch.channels_last),
-                                 layer.bias if b is None else b,
+                    h = F.conv2d(h, w, layer.bias if b is None else b,
                                  layer.stride, layer.padding, layer.dilation, layer.groups)
                 else:
                     h = layer(h)
+                i += 1
             return h.squeeze(1).squeeze(2)
         for layer in layers:
             h = layer(h)
@@ -139,6 +160,106 @@ STFT_D_HIP = True  # test switch: False keeps every STFT-discriminator conv on t
 # solvers then run without the NCHW<->NHWC batched transposes around every
 # conv (train step 104.1 -> 101.3 ms)
 STFT_D_NHWC = True
+# the element-wise glue around those convs on stftd.hip (join_to_cl,
+# bias_lrelu); False: torch's slice / copy / leaky_relu / bias launches
+STFT_D_FUSED = True
+
+
+def _lrelu_cl_ok(C: int) -> bool:
+    return C % 8 == 0 and 256 % (C // 8) == 0 and C <= 512
+
+
+def _wdt_of(t: torch.Tensor) -> int:
+    return {torch.float16: _lib.WDT_F16, torch.bfloat16: _lib.WDT_BF16}[t.dtype]
+
+
+class _JoinToCL(torch.autograd.Function):
+    """[B, C, F_out, T] channels-last = leaky_relu of the row-joined conv
+    output y [B, C, F_out * L] at columns f*L + p1 + t (conv2d_freq), one
+    kernel each way (stftd.hip join_to_cl; mrd.py:121-124 Conv2d ->
+    LeakyReLU)."""
+
+    @staticmethod
+    def forward(ctx, y, F_out: int, L: int, p1: int, T: int, slope: float):
+        B, C, FL = y.shape
+        assert FL == F_out * L and y.dtype in (torch.float16, torch.bfloat16)
+        y = y.contiguous()
+        out = torch.empty(B, F_out, T, C, device=y.device, dtype=y.dtype)
+        _lib.check(_lib.load().vits_stftd_join_to_cl_forward(
+            y.data_ptr(), out.data_ptr(), B, C, F_out, L, p1, T, slope, _wdt_of(y),
+            _stream_ptr(y.device)), "vits_stftd_join_to_cl_forward")
+        ctx.save_for_backward(out)
+        ctx.conf = (F_out, L, p1, T, slope)
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (out,) = ctx.saved_tensors
+        F_out, L, p1, T, slope = ctx.conf
+        B, _, _, C = out.shape
+        gp = g.permute(0, 2, 3, 1)
+        if not gp.is_contiguous():
+            gp = gp.contiguous()
+        gp = gp.to(out.dtype)
+        dy = torch.empty(B, C, F_out * L, device=out.device, dtype=out.dtype)
+        _lib.check(_lib.load().vits_stftd_join_to_cl_backward(
+            gp.data_ptr(), out.data_ptr(), dy.data_ptr(), B, C, F_out, L, p1, T, slope,
+            _wdt_of(out), _stream_ptr(out.device)), "vits_stftd_join_to_cl_backward")
+        return dy, None, None, None, None, None
+
+
+class _BiasLReLUCL(torch.autograd.Function):
+    """leaky_relu(y + fp16(bias), slope) on a channels-last conv output (the
+    MIOpen conv runs without bias); backward: the data gradient and the
+    bias gradient (stftd.hip bias_lrelu: one pass over the tensor, then an
+    ordered sum of its per-workgroup partials)."""
+
+    @staticmethod
+    def forward(ctx, y, bias, slope: float):
+        B, C, H, W = y.shape
+        yp = y.permute(0, 2, 3, 1)
+        if not yp.is_contiguous():
+            yp = yp.contiguous()
+        b32 = bias.detach()
+        if b32.dtype != torch.float32 or not b32.is_contiguous():
+            b32 = b32.float().contiguous()
+        out = torch.empty_like(yp)
+        _lib.check(_lib.load().vits_bias_lrelu_forward(
+            yp.data_ptr(), b32.data_ptr(), out.data_ptr(), B * H * W, C, slope, _wdt_of(yp),
+            _stream_ptr(y.device)), "vits_bias_lrelu_forward")
+        ctx.save_for_backward(out)
+        ctx.slope = slope
+        ctx.bias_dtype = bias.dtype
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (out,) = ctx.saved_tensors
+        B, H, W, C = out.shape
+        gp = g.permute(0, 2, 3, 1)
+        if not gp.is_contiguous():
+            gp = gp.contiguous()
+        gp = gp.to(out.dtype)
+        dy = torch.empty_like(out)
+        db = torch.empty(C, device=out.device, dtype=torch.float32)
+        lib = _lib.load()
+        rows = B * H * W
+        nws = int(lib.vits_bias_lrelu_workspace(rows, C))
+        ws = torch.empty(max(nws, 1), device=out.device, dtype=torch.float32)
+        _lib.check(lib.vits_bias_lrelu_backward(
+            gp.data_ptr(), out.data_ptr(), dy.data_ptr(), db.data_ptr(), ws.data_ptr(), nws,
+            rows, C, ctx.slope, _wdt_of(out), _stream_ptr(out.device)),
+            "vits_bias_lrelu_backward")
+        return (dy.permute(0, 3, 1, 2), db.to(ctx.bias_dtype) if ctx.needs_input_grad[1] else None,
+                None)
+
+
+def bias_lrelu_cl(y: torch.Tensor, bias: torch.Tensor, slope: float) -> torch.Tensor:
+    """leaky_relu(y + bias, slope) for a 16-bit channels-last Conv2d output
+    on the GPU (one HIP kernel each way); torch elsewhere."""
+    if y.device.type != "cuda" or y.dtype not in (torch.float16, torch.bfloat16):
+        return F.leaky_relu(y + bias.to(y.dtype).view(1, -1, 1, 1), slope)
+    return _BiasLReLUCL.apply(y, bias, slope)
 
 
 def _freq_conv_ok(layer) -> bool:
@@ -151,7 +272,7 @@ def _freq_conv_ok(layer) -> bool:
             and train_ops._lib_k_ok(layer.kernel_size[1], 1))
 
 
-def conv2d_freq(layer, h, wdt, in_slope: float = 1.0):
+def conv2d_freq(layer, h, wdt, in_slope: float = 1.0, out_slope: float | None = None):
     """Conv2d(C, O, (k0, k1), stride (s0, 1), padding (0, p1)) over [B, C, F, T]
     (after leaky_relu(., in_slope) when in_slope != 1) as ONE stride-1 Conv1d
     along time: the frequency windows are unfolded into channels and the F_out
@@ -182,7 +303,10 @@ def conv2d_freq(layer, h, wdt, in_slope: float = 1.0):
     u = u.permute(0, 1, 4, 2, 3).reshape(B, C * k0, F_out * L)
     w = layer.weight.reshape(O, C * k0, k1)
     y = train_ops.conv1d_hip(u, w, layer.bias, 1, p1, in_slope, wdt)  # [B, O, F_out*L]
-    return y.view(B, O, F_out, L)[..., p1:p1 + T]
+    if out_slope is not None and y.dtype in (torch.float16, torch.bfloat16):
+        return _JoinToCL.apply(y, F_out, L, p1, T, out_slope)
+    y = y.view(B, O, F_out, L)[..., p1:p1 + T]
+    return y if out_slope is None else F.leaky_relu(y, out_slope)
 
 
 class MultiSTFTDiscriminator(nn.Module):

@@ -165,12 +165,19 @@ class ResidualCouplingBlock(nn.Module):
         return list(self.flows)[::-1]
 
     def forward(self, x, x_mask, g=None, reverse=False):
-        if not reverse:
-            for flow in self.flows:
-                x, _ = flow(x, x_mask, g=g, reverse=reverse)
-        else:
-            for flow in reversed(self.flows):
-                x = flow(x, x_mask, g=g, reverse=reverse)
+        flows = list(self.flows) if not reverse else list(self.flows)[::-1]
+        i = 0
+        while i < len(flows):
+            f = flows[i]
+            # a coupling followed by a Flip: the flip folded into the coupling
+            flip = (isinstance(f, modules.ResidualCouplingLayer) and i + 1 < len(flows)
+                    and isinstance(flows[i + 1], modules.Flip))
+            kw = dict(flip=True) if flip else {}
+            if not reverse:
+                x, _ = f(x, x_mask, g=g, reverse=reverse, **kw)
+            else:
+                x = f(x, x_mask, g=g, reverse=reverse, **kw)
+            i += 2 if flip else 1
         return x
 
     @torch.no_grad()

@@ -70,7 +70,11 @@ class WN(nn.Module):
         H = self.hidden_channels
         return train_ops.gate(x_in, None if g is None else g[:, i * 2 * H:(i + 1) * 2 * H])
 
-    def forward(self, x, x_mask, g=None, **kwargs):
+    def forward(self, x, x_mask, g=None, out16=False, x16=None, **kwargs):
+        """out16: return the output rounded to the 16-bit autocast type when
+        the fused path applies (for a caller whose only use of it is an
+        autocast conv, which would round it there); x16: x already rounded
+        (train_ops.mask_cast), the first in_layer's input."""
         H = self.hidden_channels
         output = None  # zeros_like(x), materialised on first use
         g32 = None
@@ -80,7 +84,8 @@ class WN(nn.Module):
             g32 = train_ops.cond_f32(g)  # one cast for every layer's fused gate
             if g32 is not None:  # the layers' slices, with a one-launch backward
                 g32 = train_ops.split_cols(g32, self.n_layers, H2)
-        x16 = None  # x rounded to the conv dtype by the fused update (WNUpdate16)
+        # x rounded to the conv dtype (by the caller, then by WNUpdate16)
+        x16 = x16 if x16 is not None and x16.shape == x.shape else None
         for i in range(self.n_layers):
             xi = x if x16 is None else x16
             g_l = g[:, i * H2:(i + 1) * H2] if self.gin_channels else None
@@ -105,6 +110,11 @@ class WN(nn.Module):
                     x = (x + rs[:, :H]) * x_mask
                     output = (torch.zeros_like(x) if output is None else output) + rs[:, H:]
             else:
+                if out16:
+                    # (output + rs) * x_mask, rounded for the consuming conv
+                    o16 = train_ops.wn_final(output, rs, x_mask)
+                    if o16 is not None:
+                        return o16
                 output = (torch.zeros_like(x) if output is None else output) + rs
         return output * x_mask
 
@@ -207,14 +217,40 @@ class ResidualCouplingLayer(nn.Module):
             m, logs = stats, torch.zeros_like(stats)
         return m, logs
 
-    def forward(self, x, x_mask, g=None, reverse=False):
+    def _fused(self, x, x_mask, g, reverse, flip):
+        """The mean-only coupling on the fused fp16 training path: pre conv ->
+        mask_cast (h and the first in_layer's 16-bit input) -> WN (16-bit
+        output) -> post conv -> one coupling-update kernel (+ the Flip that
+        follows, when ``flip``).  None where it does not apply."""
+        if not (self.mean_only and train_ops.coupling_fused_ok(x, x_mask)):
+            return None
+        x0 = x[:, :self.half_channels]
+        y = train_ops.conv1d(self.pre, x0)
+        mc = train_ops.mask_cast(y, x_mask)
+        if mc is None:
+            return None
+        h, h16 = mc
+        o = self.enc(h, x_mask, g=g, out16=True, x16=h16)
+        p = train_ops.conv1d(self.post, o)
+        return train_ops.coupling_update(x, p, x_mask, reverse, flip)
+
+    def forward(self, x, x_mask, g=None, reverse=False, flip=False):
+        """flip: apply the following Flip module's channel reversal to the
+        result (ResidualCouplingBlock folds it into the update kernel)."""
+        out = self._fused(x, x_mask, g, reverse, flip)
+        if out is not None:
+            if reverse:
+                return out
+            return out, torch.zeros(x.shape[0], device=x.device, dtype=x.dtype)
         x0, x1 = torch.split(x, [self.half_channels] * 2, 1)
         m, logs = self._stats(x0, x_mask, g)
         if not reverse:
             x1 = m + x1 * torch.exp(logs) * x_mask
-            return torch.cat([x0, x1], 1), torch.sum(logs, [1, 2])
+            out, logdet = torch.cat([x0, x1], 1), torch.sum(logs, [1, 2])
+            return (torch.flip(out, [1]) if flip else out), logdet
         x1 = (x1 - m) * torch.exp(-logs) * x_mask
-        return torch.cat([x0, x1], 1)
+        out = torch.cat([x0, x1], 1)
+        return torch.flip(out, [1]) if flip else out
 
     def infer(self, x, g, reverse=True):
         from .engine import coupling_infer

@@ -713,6 +713,157 @@ def wn_update(x: torch.Tensor, rs: torch.Tensor, mask: torch.Tensor, out):
                             None if out is None else out.contiguous(), wdt)
 
 
+def _coupling_ok(wdt, *tensors16) -> bool:
+    return (wdt is not None and _io16(wdt) and COUPLING_FUSED
+            and all(t.dtype == _TORCH_16[wdt] for t in tensors16))
+
+
+# the coupling layers' element-wise glue on wnres.hip (mask_cast, wn_final,
+# coupling); False: the reference's torch ops
+COUPLING_FUSED = True
+
+
+def _mask_ok(mask: torch.Tensor, B: int, T: int) -> bool:
+    return (mask.dtype == torch.float32 and mask.is_contiguous()
+            and tuple(mask.shape) == (B, 1, T))
+
+
+class MaskCast16(torch.autograd.Function):
+    """(y * mask, the same rounded to the 16-bit type) for a 16-bit conv
+    output y and an fp32 mask - the coupling's ``pre(x0) * x_mask`` and the
+    WN's first in_layer input (csrc/wnres.hip mask_cast)."""
+
+    @staticmethod
+    def forward(ctx, y, mask, wdtype: int):
+        B, C, T = y.shape
+        y = y.contiguous()
+        h = torch.empty(B, C, T, device=y.device, dtype=torch.float32)
+        h16 = torch.empty_like(y)
+        check(_lib.load().vits_mask_cast_forward(
+            y.data_ptr(), mask.data_ptr(), h.data_ptr(), h16.data_ptr(), B, C, T, wdtype,
+            _stream_ptr(y.device)), "vits_mask_cast_forward")
+        ctx.save_for_backward(mask)
+        ctx.conf = (B, C, T, wdtype, y.dtype)
+        ctx.set_materialize_grads(False)
+        return h, h16
+
+    @staticmethod
+    def backward(ctx, gh, gh16):
+        (mask,) = ctx.saved_tensors
+        B, C, T, wdtype, dt = ctx.conf
+        dy = torch.empty(B, C, T, device=mask.device, dtype=dt)
+        gh = None if gh is None else gh.float().contiguous()
+        gh16 = None if gh16 is None else gh16.to(dt).contiguous()
+        check(_lib.load().vits_mask_cast_backward(
+            None if gh is None else gh.data_ptr(), None if gh16 is None else gh16.data_ptr(),
+            mask.data_ptr(), dy.data_ptr(), B, C, T, wdtype, _stream_ptr(mask.device)),
+            "vits_mask_cast_backward")
+        return dy, None, None
+
+
+def mask_cast(y: torch.Tensor, mask: torch.Tensor):
+    """(y * mask fp32, its 16-bit copy) on the fused path, else None."""
+    wdt = train_wdtype(y)
+    if not (_coupling_ok(wdt, y) and _mask_ok(mask, y.shape[0], y.shape[2])):
+        return None
+    return MaskCast16.apply(y, mask, wdt)
+
+
+class WNFinal16(torch.autograd.Function):
+    """16-bit((out + rs) * mask): the WN output (modules.py:182) for a
+    consumer that feeds it to an autocast conv (csrc/wnres.hip wn_final)."""
+
+    @staticmethod
+    def forward(ctx, out, rs, mask, wdtype: int):
+        B, C, T = rs.shape
+        rs = rs.contiguous()
+        o16 = torch.empty_like(rs)
+        check(_lib.load().vits_wn_final_forward(
+            None if out is None else out.data_ptr(), rs.data_ptr(), mask.data_ptr(),
+            o16.data_ptr(), B, C, T, wdtype, _stream_ptr(rs.device)), "vits_wn_final_forward")
+        ctx.save_for_backward(mask)
+        ctx.conf = (B, C, T, wdtype, rs.dtype, out is not None)
+        return o16
+
+    @staticmethod
+    def backward(ctx, g16):
+        (mask,) = ctx.saved_tensors
+        B, C, T, wdtype, dt, has_out = ctx.conf
+        g16 = g16.to(dt).contiguous()
+        dout = (torch.empty(B, C, T, device=mask.device, dtype=torch.float32)
+                if has_out and ctx.needs_input_grad[0] else None)
+        drs = torch.empty(B, C, T, device=mask.device, dtype=dt)
+        check(_lib.load().vits_wn_final_backward(
+            g16.data_ptr(), mask.data_ptr(), None if dout is None else dout.data_ptr(),
+            drs.data_ptr(), B, C, T, wdtype, _stream_ptr(mask.device)), "vits_wn_final_backward")
+        return dout, drs, None, None
+
+
+def wn_final(out, rs: torch.Tensor, mask: torch.Tensor):
+    """16-bit((out + rs) * mask) on the fused path (out fp32 or None), else
+    None."""
+    wdt = train_wdtype(rs)
+    if not (_coupling_ok(wdt, rs) and _mask_ok(mask, rs.shape[0], rs.shape[2])):
+        return None
+    if out is not None:
+        if out.dtype != torch.float32 or out.shape != rs.shape:
+            return None
+        out = out.contiguous()
+    return WNFinal16.apply(out, rs, mask, wdt)
+
+
+class Coupling16(torch.autograd.Function):
+    """The mean-only coupling update (modules.py:352-360 with logs = 0):
+    cat(x0, m + x1 * mask) forward, cat(x0, (x1 - m) * mask) reverse, m =
+    p * mask for the 16-bit post-conv output p; optionally channel-flipped
+    (the Flip that follows, models.py:219-235).  csrc/wnres.hip coupling."""
+
+    @staticmethod
+    def forward(ctx, x, p, mask, reverse: bool, flip: bool, wdtype: int):
+        B, C2, T = x.shape
+        half = C2 // 2
+        x = x.contiguous()
+        p = p.contiguous()
+        out = torch.empty_like(x)
+        check(_lib.load().vits_coupling_forward(
+            x.data_ptr(), p.data_ptr(), mask.data_ptr(), out.data_ptr(), B, half, T, int(reverse),
+            int(flip), wdtype, _stream_ptr(x.device)), "vits_coupling_forward")
+        ctx.save_for_backward(mask)
+        ctx.conf = (B, half, T, int(reverse), int(flip), wdtype, p.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (mask,) = ctx.saved_tensors
+        B, half, T, reverse, flip, wdtype, dt = ctx.conf
+        g = g.float().contiguous()
+        gx = torch.empty(B, 2 * half, T, device=g.device, dtype=torch.float32)
+        gp = torch.empty(B, half, T, device=g.device, dtype=dt)
+        check(_lib.load().vits_coupling_backward(
+            g.data_ptr(), mask.data_ptr(), gx.data_ptr(), gp.data_ptr(), B, half, T, reverse, flip,
+            wdtype, _stream_ptr(g.device)), "vits_coupling_backward")
+        return gx, gp, None, None, None, None
+
+
+def coupling_fused_ok(x: torch.Tensor, mask: torch.Tensor) -> bool:
+    """Whether a coupling on x (fp32 [B, 2h, T]) takes the fused path."""
+    wdt = train_wdtype(x)
+    return (_coupling_ok(wdt) and x.dtype == torch.float32 and x.dim() == 3
+            and _mask_ok(mask, x.shape[0], x.shape[2]))
+
+
+def coupling_update(x: torch.Tensor, p: torch.Tensor, mask: torch.Tensor, reverse: bool,
+                    flip: bool):
+    """Coupling16 on the fused path (x fp32 [B, 2h, T], p 16-bit [B, h, T]),
+    else None."""
+    wdt = train_wdtype(x)
+    if not (_coupling_ok(wdt, p) and x.dtype == torch.float32
+            and _mask_ok(mask, x.shape[0], x.shape[2])
+            and tuple(p.shape) == (x.shape[0], x.shape[1] // 2, x.shape[2])):
+        return None
+    return Coupling16.apply(x, p, mask, reverse, flip, wdt)
+
+
 # 16-bit activations for the training convs / gates under fp16 autocast (the
 # reference's autocast convs return fp16); False: the fp32-I/O kernels
 TRAIN_IO16 = True
