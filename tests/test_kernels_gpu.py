@@ -241,8 +241,13 @@ def test_conv_post_tanh(device, T, dt):
     _close(out, ref, what="conv_post")
 
 
-@pytest.mark.parametrize("B,Tt,Ts", [(4, 60, 13), (3, 500, 100), (2, 1000, 384), (1, 7, 7), (2, 300, 65)])
+@pytest.mark.parametrize("B,Tt,Ts", [(4, 60, 13), (3, 500, 100), (2, 1000, 384), (1, 7, 7),
+                                     (2, 300, 65), (5, 33, 17), (3, 64, 40), (3, 65, 64),
+                                     (1, 1, 1), (64, 500, 100)])
 def test_maximum_path_bitexact(device, B, Tt, Ts):
+    """vits_maximum_path vs the C oracle (core.pyx restated), bit-exact:
+    ragged lengths, 32-row decision-word block edges (33, 64, 65 rows), the
+    global-workspace decision words (1000 x 384) and the benchmark shape."""
     from oracle import mas as mas_oracle
 
     rng = np.random.default_rng(Tt * 7 + Ts)

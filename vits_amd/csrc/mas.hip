@@ -22,11 +22,16 @@
 //  * waves 1-3 stream the next chunk of neg_cent rows (R rows, coalesced)
 //    into an LDS double buffer while wave 0 consumes the current one, one
 //    barrier per chunk;
-//  * the backtrack decision for (y, x) is V[y-1][x] < V[y-1][x-1]; wave 0
-//    produces it for a whole row with one ballot per register column and
-//    keeps the bits in LDS (global workspace when they do not fit), so the
-//    sequential backtrack reads one bit per row from LDS;
+//  * the backtrack decision for (y, x) is V[y-1][x] < V[y-1][x-1]; each lane
+//    ORs it into a register word per column (bit y mod 32) and stores the
+//    words once per 32 rows (LDS, or the global workspace when they do not
+//    fit): no per-row ballot, SALU hop or LDS store on the DP's chain;
+//  * the backtrack runs on wave 0: per 32-row block, lane l holds the
+//    decision word of column index - l (the path moves at most one column
+//    per row), and each row is a readlane + bit test - no memory latency
+//    per row;
 //  * the path is written in one coalesced pass from the per-row column index.
+// (Round 5: per-row ballots + a one-lane backtrack, 194 us at B=64, 500 x 100.)
 #include "common.h"
 
 namespace {
@@ -95,7 +100,7 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
                                                   const int32_t* __restrict__ tt_len,
                                                   const int32_t* __restrict__ ts_len, void* path,
                                                   int path_dt, int T_t, int T_s,
-                                                  uint64_t* __restrict__ bits_global,
+                                                  uint32_t* __restrict__ bits_global,
                                                   int bits_in_lds) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int b = blockIdx.x;
@@ -107,14 +112,15 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
   const int R = mas_rows(XPL);
   float* ring = reinterpret_cast<float*>(smem_raw);             // [2][R][W]
   int32_t* idx_row = reinterpret_cast<int32_t*>(ring + 2 * R * W);  // [T_t]
-  // compile-time address space for the decision bits: LDS (ds_read/write)
-  // or the global workspace -- a runtime select would make every access a
-  // FLAT op waiting on both counters
-  uint64_t* bits;
+  // decision words [ceil(T_t / 32)][W]: bit (y mod 32) of word (y / 32, x).
+  // Compile-time address space: LDS (ds_read/write) or the global workspace
+  // -- a runtime select would make every access a FLAT op waiting on both
+  // counters
+  uint32_t* bits;
   if constexpr (BITS_LDS)
-    bits = reinterpret_cast<uint64_t*>(idx_row + ((T_t + 1) & ~1));
+    bits = reinterpret_cast<uint32_t*>(idx_row + ((T_t + 3) & ~3));
   else
-    bits = bits_global + (int64_t)b * T_t * XPL;
+    bits = bits_global + (int64_t)b * ((T_t + 31) >> 5) * W;
 
   int t_t = tt_len[b];
   int t_s = ts_len[b];
@@ -147,8 +153,22 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
   __syncthreads();
 
   float vp[XPL];
+  uint32_t dw[XPL];  // this lane's decision words of the current 32-row block
+  // the DP band: cell (y, x) is updated iff lo <= x < hi, lo = max(0, t_s +
+  // y - t_t), hi = min(t_s, y + 1), i.e. iff 0 <= y - x <= D = t_t - t_s
+  // and x < t_s: one unsigned compare of y - xs against D, with xs = x, or
+  // a value no y reaches for columns outside [0, t_s) (and every column
+  // when t_s > t_t: then no cell is updated)
+  const int D = t_t - t_s;
+  const uint32_t Du = D < 0 ? 0u : (uint32_t)D;
+  int xs[XPL];
 #pragma unroll
-  for (int i = 0; i < XPL; ++i) vp[i] = 0.f;
+  for (int i = 0; i < XPL; ++i) {
+    vp[i] = 0.f;
+    dw[i] = 0u;
+    const int x = lane * XPL + i;
+    xs[i] = (x < t_s && D >= 0) ? x : 0x40000000;
+  }
   const int xbase = lane * XPL;
 
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -158,67 +178,85 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ neg_
       const float* rows = ring + (ch & 1) * R * W;
       const int y0 = ch * R;
       const int yend = min(t_t, y0 + R);
-      // the next row's scores are read from LDS while this row computes
-      float nxt[XPL];
-      if (y0 < yend) {
+      // two row registers, no moves between them: row y + 2's scores are
+      // read into ra right after row y consumed it, i.e. one row of work
+      // ahead of their use (reads past the chunk's last row land in
+      // allocated LDS and are never used)
+      float ra[XPL], rb[XPL];
+      auto rd = [&](float* r, int y) {
+        const float* src = rows + (y - y0) * W + xbase;
 #pragma unroll
-        for (int i = 0; i < XPL; ++i) nxt[i] = rows[xbase + i];
-      }
-      for (int y = y0; y < yend; ++y) {
-        float cur[XPL];
-#pragma unroll
-        for (int i = 0; i < XPL; ++i) cur[i] = nxt[i];
-        if (y + 1 < yend) {
-          const float* rown = rows + (y + 1 - y0) * W + xbase;
-#pragma unroll
-          for (int i = 0; i < XPL; ++i) nxt[i] = rown[i];
-        }
-        const int lo = max(0, t_s + y - t_t);
-        const int hi = min(t_s, y + 1);
+        for (int i = 0; i < XPL; ++i) r[i] = src[i];
+      };
+      auto row = [&](int y, const float* cur) {
         // column x-1 of this lane's first element: lane-1's last register,
-        // one DPP wave shift (no LDS round trip; lane 0 never uses it)
-        const float left = __int_as_float(
-            __builtin_amdgcn_update_dpp(0, __float_as_int(vp[XPL - 1]), 0x138, 0xf, 0xf, false));
+        // one DPP wave shift; lane 0 (x = 0) receives the DP's left
+        // boundary V[y-1][-1] = (y == 0 ? 0 : -1e9) as the shift's fill
+        const float bnd = y == 0 ? 0.f : MAS_NEG;
+        const float left = __int_as_float(__builtin_amdgcn_update_dpp(
+            __float_as_int(bnd), __float_as_int(vp[XPL - 1]), 0x138, 0xf, 0xf, false));
+        const uint32_t bit = 1u << (y & 31);
         float vn[XPL];
 #pragma unroll
         for (int i = 0; i < XPL; ++i) {
-          const int x = xbase + i;
           const float vcur_raw = vp[i];
           const float vprev_raw = (i == 0) ? left : vp[i - 1];
-          // decision bit for the backtrack at (y, x): V[y-1][x] < V[y-1][x-1]
-          const bool dec = (y >= 1) && (x >= 1) && (vcur_raw < vprev_raw);
-          const unsigned long long m = __ballot(dec);
-          if (lane == 0) bits[(int64_t)y * XPL + i] = m;
-          float v = cur[i];
-          if (x >= lo && x < hi) {
-            const float v_cur = (x == y) ? MAS_NEG : vcur_raw;
-            const float v_prev = (x == 0) ? (y == 0 ? 0.f : MAS_NEG) : vprev_raw;
-            const float mx = (v_cur > v_prev) ? v_cur : v_prev;  // Cython max(v_prev, v_cur)
-            v = v + mx;
-          }
-          vn[i] = v;
+          // backtrack decision at (y, x): V[y-1][x] < V[y-1][x-1]
+          // (consulted only for y >= 1, x >= 1)
+          dw[i] |= (vcur_raw < vprev_raw) ? bit : 0u;
+          const uint32_t dy = (uint32_t)(y - xs[i]);
+          const float v_cur = dy == 0u ? MAS_NEG : vcur_raw;         // x == y
+          const float mx = (v_cur > vprev_raw) ? v_cur : vprev_raw;  // Cython max(v_prev, v_cur)
+          const float upd = cur[i] + mx;
+          vn[i] = dy <= Du ? upd : cur[i];
         }
 #pragma unroll
         for (int i = 0; i < XPL; ++i) vp[i] = vn[i];
+        if ((y & 31) == 31 || y == t_t - 1) {  // block of 32 rows complete
+#pragma unroll
+          for (int i = 0; i < XPL; ++i) {
+            bits[(int64_t)(y >> 5) * W + xbase + i] = dw[i];
+            dw[i] = 0u;
+          }
+        }
+      };
+      rd(ra, y0);
+      rd(rb, y0 + 1);
+      for (int y = y0; y < yend; y += 2) {
+        row(y, ra);
+        rd(ra, y + 2);
+        if (y + 1 < yend) {
+          row(y + 1, rb);
+          rd(rb, y + 3);
+        }
       }
     }
     __syncthreads();
   }
 
-  // ---- backtrack (one lane) -------------------------------------------------
-  if (tid == 0) {
+  // ---- backtrack (wave 0) ---------------------------------------------------
+  // index is wave-uniform; per 32-row block lane l < 32 holds the decision
+  // word of column top - l, top = index at the block's last row
+  if (wid == 0 && t_t > 0 && t_s > 0) {
     int index = t_s - 1;
-    for (int y = t_t - 1; y >= 0; --y) {
-      idx_row[y] = index;
-      if (index != 0) {
-        bool dec = (index == y);
-        if (!dec && y >= 1 && index >= 0) {
-          const int l = index / XPL;
-          const int i = index - l * XPL;
-          dec = (bits[(int64_t)y * XPL + i] >> l) & 1ull;
+    int my_idx = 0;  // lane l: the path column of row 32 * blk + l
+    for (int blk = (t_t - 1) >> 5; blk >= 0; --blk) {
+      const int top = index;
+      const int col = top - lane;
+      const uint32_t wv = (lane < 32 && col >= 0) ? bits[(int64_t)blk * W + col] : 0u;
+      const int yhi = min(t_t - 1, blk * 32 + 31);
+      for (int y = yhi; y >= blk * 32; --y) {
+        my_idx = (lane == (y & 31)) ? index : my_idx;
+        if (index != 0) {
+          bool dec = (index == y);
+          if (!dec && y >= 1) {
+            const uint32_t w = __builtin_amdgcn_readlane(wv, top - index);
+            dec = (w >> (y & 31)) & 1u;
+          }
+          if (dec) index = index - 1;
         }
-        if (dec) index = index - 1;
       }
+      if (lane < 32 && blk * 32 + lane <= yhi) idx_row[blk * 32 + lane] = my_idx;
     }
   }
   __syncthreads();
@@ -240,22 +278,26 @@ int pick_xpl(int t_s) {
   return xpl;
 }
 
-size_t bits_bytes(int t_t, int xpl) { return (size_t)t_t * xpl * sizeof(uint64_t); }
+size_t bits_bytes(int t_t, int xpl) {
+  return (size_t)((t_t + 31) / 32) * 64 * xpl * sizeof(uint32_t);
+}
 
 int mas_run(const float* neg_cent, const int32_t* tt, const int32_t* ts, void* path, int path_dt,
             int batch, int T_t, int T_s, void* workspace, int64_t ws_bytes, hipStream_t s) {
   const int xpl = pick_xpl(T_s);
   if (xpl > 32) return VITS_E_UNSUP;
   const size_t ring = sizeof(float) * 2 * mas_rows(xpl) * 64 * xpl;
-  const size_t idx = sizeof(int32_t) * ((T_t + 1) & ~1);
+  const size_t idx = sizeof(int32_t) * ((T_t + 3) & ~3);
   const size_t bb = bits_bytes(T_t, xpl);
   int in_lds = bb <= (size_t)MAS_BITS_LDS_MAX && ring + idx + bb <= 150 * 1024;
   size_t lds = ring + idx + (in_lds ? bb : 0);
-  uint64_t* gbits = nullptr;
+  uint32_t* gbits = nullptr;
   if (!in_lds) {
     if (!workspace || ws_bytes < (int64_t)(bb * batch)) return VITS_E_ARG;
-    gbits = reinterpret_cast<uint64_t*>(workspace);
+    gbits = reinterpret_cast<uint32_t*>(workspace);
   }
+  // (three rows of slack past the ring: the DP reads up to 3 rows ahead)
+  lds += sizeof(float) * 3 * 64 * xpl;
   if (lds > 160 * 1024) return VITS_E_UNSUP;
   dim3 grid(batch), block(256);
 #define MAS_CASE(X)                                                                         \
@@ -287,7 +329,7 @@ extern "C" int64_t vits_maximum_path_workspace(int batch, int t_t, int t_s) {
   if (batch <= 0 || t_t <= 0 || t_s <= 0) return 0;
   const int xpl = pick_xpl(t_s);
   const size_t ring = sizeof(float) * 2 * mas_rows(xpl) * 64 * xpl;
-  const size_t idx = sizeof(int32_t) * ((t_t + 1) & ~1);
+  const size_t idx = sizeof(int32_t) * ((t_t + 3) & ~3);
   const size_t bb = bits_bytes(t_t, xpl);
   const bool in_lds = bb <= (size_t)MAS_BITS_LDS_MAX && ring + idx + bb <= 150 * 1024;
   // always reserve room for the two length vectors of vits_maximum_path
