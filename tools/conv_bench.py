@@ -17,6 +17,9 @@ for st, (C, T) in enumerate([(256, 8 * Ty), (128, 48 * Ty), (64, 96 * Ty), (32, 
         shapes.append((f"s{st}.c2.k{k}", C // 2, C, k, 1, T, False, None))
 shapes.append(("flow.in", 256, 512, 5, 1, Ty, True, None))
 shapes.append(("flow.rs", 256, 512, 1, 1, Ty, False, None))
+shapes.append(("flow.rsl", 256, 256, 1, 1, Ty, False, None))
+shapes.append(("flow.post", 256, 96, 1, 1, Ty, False, None))
+shapes.append(("flow.pre", 96, 256, 1, 1, Ty, False, None))
 shapes.append(("up0", 512, 256, 16, 1, Ty, False, (8, 16)))
 shapes.append(("up1", 256, 128, 12, 1, 8 * Ty, False, (6, 12)))
 shapes.append(("pre", 192, 512, 7, 1, Ty, False, None))
@@ -28,6 +31,8 @@ CHECK = os.environ.get("CHECK", "0") == "1"  # error vs the exact-f32 kernel and
 tiles = [int(t) for t in os.environ.get("TILES", "").split(",") if t]
 kcms = [int(t) for t in os.environ.get("KCM", "1").split(",") if t]
 reps = int(os.environ.get("REPS", "5"))
+if os.environ.get("SPLITW"):  # 0: split fp32 with in-kernel weight splits (F32S)
+    ops.SPLIT_W = os.environ["SPLITW"] == "1"
 if os.environ.get("F32P_KC"):  # chunk channels of the split-fp32 128-row tiles (32 / 16)
     ops.F32P_MAX_KC = int(os.environ["F32P_KC"])
 tot_fl, tot_ms = 0, 0

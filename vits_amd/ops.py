@@ -244,8 +244,11 @@ def _kc_f32p(cin_pad: int, k: int, dil: int, tile: int) -> int:
         # 64-row layers (the 64-channel decoder stage): 16-channel chunks halve
         # the double-buffered window (3 instead of 2 workgroups per CU);
         # measured on MI355X (tools/conv_bench.py WDT=3, r03): c1 k=3/7/11
-        # +15/+8/+3 %, c2 +12..17 % over 32-channel chunks
-        return 16
+        # +15/+8/+3 %, c2 +12..17 % over 32-channel chunks.  A 1x1 layer's
+        # window is one tile wide, and its chunks are latency-bound: 32
+        # channels (the flow's 96-row post conv: 29.5 -> 21.6 us, r06; the
+        # k-steps and so the accumulation order are the same either way)
+        return 32 if (k == 1 and cin_pad % 32 == 0) else 16
     bn = TILE_COLS[tile]
     xrs = (bn + (k - 1) * dil + 3 + 3) // 4 * 4  # window row incl. the 16-byte alignment shift
     budget = 6144 if bn <= 128 else 10240
