@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--replays", type=int, default=1)
     a = ap.parse_args()
+    torch.backends.cudnn.benchmark = True  # as bench.py's train legs (train_stft.py:26)
     from vits_amd.train import TrainStep, build_models, default_hps, synthetic_batch
 
     dev = torch.device("cuda:0")
