@@ -7,6 +7,10 @@ B=${2:-32}
 OUT=gpurun_out/prof_${TAG}_train
 export TMPDIR=/tmp
 mkdir -p $OUT
+# one unprofiled run first: MIOpen's exhaustive find (cudnn.benchmark, as the
+# bench) writes the box's find-db, so every profiled run below starts from
+# the same db and R=2 - R=1 cancels the search
+timeout -k 10 300 python3 tools/train_pmc.py --batch $B --replays 1 > $OUT/warm.log 2>&1
 for R in 1 2; do
   echo "pass R=$R"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace$R -o run -- \
