@@ -684,7 +684,8 @@ int vits_coupling_backward(const float* g, const float* mask, float* gx, void* g
 /* bias_lrelu: out = leaky_relu(y + fp16(bias), slope) on NHWC rows of C  */
 /* channels (the MIOpen conv runs without bias); backward: dy = lrelu'(out)*g */
 /* and db[c] = fp16-rounded fp32 sum of dy (deterministic: per-workgroup  */
-/* partials in `workspace`, added in workgroup order by a second launch). */
+/* partials in `workspace`, added in workgroup order by a second launch; */
+/* db NULL: the data gradient only, one launch, no workspace).           */
 /* 16-bit tensors of `wdtype`; C % 8 == 0, C <= 512 (bias_lrelu backward: */
 /* 256 % (C/8) == 0).                                                      */
 /* ---------------------------------------------------------------------- */

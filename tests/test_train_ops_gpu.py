@@ -758,6 +758,10 @@ def test_bias_lrelu_cl(device, B, C, H, W):
     bias.grad = None
     D.bias_lrelu_cl(y.clone().requires_grad_(True), bias, 0.2).backward(dy)
     assert torch.equal(bias.grad, g1)
+    # the bias not requiring a gradient: the data gradient alone, unchanged
+    yd2 = y.clone().requires_grad_(True)
+    D.bias_lrelu_cl(yd2, bias.detach(), 0.2).backward(dy)
+    assert torch.equal(yd2.grad, yr.grad)
 
 
 @pytest.mark.parametrize("reverse", [False, True])

@@ -225,6 +225,7 @@ __global__ __launch_bounds__(256) void bias_lrelu_bwd_kernel(
       }
     }
   }
+  if (!partial) return;  // (data gradient only: no bias gradient wanted)
 #pragma unroll
   for (int i = 0; i < 8; ++i) red[tid * 8 + i] = acc[i];
   __syncthreads();
@@ -319,25 +320,28 @@ extern "C" int vits_bias_lrelu_workspace(int64_t rows, int C) {
 extern "C" int vits_bias_lrelu_backward(const void* g, const void* out, void* dy, float* db,
                                         float* workspace, int ws_floats, int64_t rows, int C,
                                         float slope, int wdtype, void* stream) {
-  VITS_CHECK_ARG(g && out && dy && db && workspace && rows > 0 && C > 0);
+  VITS_CHECK_ARG(g && out && dy && rows > 0 && C > 0 && (!db || workspace));
   VITS_CHECK_ARG(C % 8 == 0 && 256 % (C / 8) == 0 && C <= 512);
   VITS_CHECK_ARG(wdtype == VITS_WDT_F16 || wdtype == VITS_WDT_BF16);
   const int need = vits_bias_lrelu_workspace(rows, C);
-  VITS_CHECK_ARG(ws_floats >= need);
+  VITS_CHECK_ARG(!db || ws_floats >= need);
   const int nb = need / C;
+  if (!db) workspace = nullptr;  // db NULL: the data gradient only, one launch
   hipStream_t s = as_stream(stream);
   if (wdtype == VITS_WDT_F16) {
     hipLaunchKernelGGL(bias_lrelu_bwd_kernel<_Float16>, dim3(nb), dim3(256), 0, s,
                        (const _Float16*)g, (const _Float16*)out, (_Float16*)dy, workspace, C,
                        rows, slope);
-    hipLaunchKernelGGL(bias_lrelu_db_kernel<_Float16>, dim3(1), dim3(256), 0, s, workspace, db,
-                       C, nb);
+    if (db)
+      hipLaunchKernelGGL(bias_lrelu_db_kernel<_Float16>, dim3(1), dim3(256), 0, s, workspace, db,
+                         C, nb);
   } else {
     hipLaunchKernelGGL(bias_lrelu_bwd_kernel<__bf16>, dim3(nb), dim3(256), 0, s,
                        (const __bf16*)g, (const __bf16*)out, (__bf16*)dy, workspace, C, rows,
                        slope);
-    hipLaunchKernelGGL(bias_lrelu_db_kernel<__bf16>, dim3(1), dim3(256), 0, s, workspace, db, C,
-                       nb);
+    if (db)
+      hipLaunchKernelGGL(bias_lrelu_db_kernel<__bf16>, dim3(1), dim3(256), 0, s, workspace, db,
+                         C, nb);
   }
   return vits_launch_status();
 }

@@ -241,17 +241,20 @@ class _BiasLReLUCL(torch.autograd.Function):
             gp = gp.contiguous()
         gp = gp.to(out.dtype)
         dy = torch.empty_like(out)
-        db = torch.empty(C, device=out.device, dtype=torch.float32)
+        want_db = ctx.needs_input_grad[1]  # (False in the generator's pass through D)
         lib = _lib.load()
         rows = B * H * W
-        nws = int(lib.vits_bias_lrelu_workspace(rows, C))
-        ws = torch.empty(max(nws, 1), device=out.device, dtype=torch.float32)
+        db = ws = None
+        nws = 0
+        if want_db:
+            db = torch.empty(C, device=out.device, dtype=torch.float32)
+            nws = int(lib.vits_bias_lrelu_workspace(rows, C))
+            ws = torch.empty(max(nws, 1), device=out.device, dtype=torch.float32)
         _lib.check(lib.vits_bias_lrelu_backward(
-            gp.data_ptr(), out.data_ptr(), dy.data_ptr(), db.data_ptr(), ws.data_ptr(), nws,
-            rows, C, ctx.slope, _wdt_of(out), _stream_ptr(out.device)),
-            "vits_bias_lrelu_backward")
-        return (dy.permute(0, 3, 1, 2), db.to(ctx.bias_dtype) if ctx.needs_input_grad[1] else None,
-                None)
+            gp.data_ptr(), out.data_ptr(), dy.data_ptr(), None if db is None else db.data_ptr(),
+            None if ws is None else ws.data_ptr(), nws, rows, C, ctx.slope, _wdt_of(out),
+            _stream_ptr(out.device)), "vits_bias_lrelu_backward")
+        return (dy.permute(0, 3, 1, 2), db.to(ctx.bias_dtype) if want_db else None, None)
 
 
 def bias_lrelu_cl(y: torch.Tensor, bias: torch.Tensor, slope: float) -> torch.Tensor:
