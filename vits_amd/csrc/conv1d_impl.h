@@ -337,6 +337,7 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
 
   // ---- W chunk: LDS-DMA, one 1 KiB piece (256 floats) per wave instruction;
   // lane l of piece q lands at LDS float q*256 + 4l (lane-linear image)
+  const float inv_c8n = 1.0f / (float)(kc >> 3);
   auto wdma = [&](int c0, float* st) {
     // the chunk's W image is R rows of L float slots, HBM row stride S:
     //   f32:  [kc*k][BM] rows of W[c][j][m0..m0+BM)
@@ -353,11 +354,16 @@ __global__ __launch_bounds__(256, (WT == VITS_WDT_F32S || WT == VITS_WDT_F32P) ?
     for (int q = wid; q < pieces; q += 4) {
       const int e = q * 256 + lane * 4;
       if (e < wsz) {
-        const int r = e / L;
+        const int r = e / L;  // (L a power-of-two constant: a shift)
         const int col = e - r * L;
         int gr = r;
         if (BF) {
-          const int j = r / c8n;
+          // r / c8n as a float product: r < 2^10 and c8n <= 8 keep
+          // (r + 0.5) / c8n >= 1/16 from an integer, far above the product's
+          // rounding, so the floor is exact - ~3 VALU instead of the ~12 of
+          // the integer division, per piece of every chunk (the training
+          // convs' chunk loop is VALU-bound)
+          const int j = (int)(((float)r + 0.5f) * inv_c8n);
           const int c8 = r - j * c8n;
           gr = ((c8 >> 1) * k + j) * 2 + (c8 & 1);
         }
